@@ -1,0 +1,121 @@
+"""ctypes binding of libclipembed.so (the C ABI declared in include/clipembed.h).
+
+The shared library is built in-tree (``make -C clip-embeds_amd``) next to this file.  There is
+no fallback: if the library is missing or cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libclipembed.so")
+
+CE_OK, CE_ERR_INVALID, CE_ERR_HIP, CE_ERR_STATE, CE_ERR_OOM = 0, 1, 2, 3, 4
+CE_F32, CE_BF16, CE_F16, CE_I64, CE_I32 = 0, 1, 2, 3, 4
+CE_ACT_GELU_ERF, CE_ACT_QUICK_GELU = 0, 1
+CE_PACL_ONES, CE_PACL_SIGMOID10 = 0, 1
+CE_ROPE_NONE, CE_ROPE_BEFORE, CE_ROPE_AFTER = 0, 1, 2
+
+
+class TowerConfig(ctypes.Structure):
+    _fields_ = [("width", c_int), ("layers", c_int), ("heads", c_int), ("mlp_width", c_int)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("embed_dim", c_int),
+        ("activation", c_int),
+        ("image_size", c_int),
+        ("patch_size", c_int),
+        ("vision", TowerConfig),
+        ("context_length", c_int),
+        ("vocab_size", c_int),
+        ("text", TowerConfig),
+        ("pacl_dim", c_int),
+    ]
+
+
+class Tensor(ctypes.Structure):
+    _fields_ = [
+        ("name", c_char_p),
+        ("data", c_void_p),
+        ("dtype", c_int),
+        ("ndim", c_int),
+        ("shape", c_int64 * 4),
+    ]
+
+
+class ClipEmbedError(RuntimeError):
+    """Raised when a libclipembed call returns a non-zero status."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"libclipembed error {status}: {message}")
+        self.status = status
+
+
+# name -> (restype, argtypes); this list is the exported surface of include/clipembed.h
+_SIGNATURES = {
+    "ce_last_error": (c_char_p, []),
+    "ce_version": (c_char_p, []),
+    "ce_create": (c_int, [POINTER(Config), c_int, POINTER(c_void_p)]),
+    "ce_destroy": (c_int, [c_void_p]),
+    "ce_load_weights": (c_int, [c_void_p, POINTER(Tensor), c_int, c_int]),
+    "ce_missing_weights": (c_int, [c_void_p, POINTER(c_int), POINTER(c_char_p)]),
+    "ce_reserve": (c_int, [c_void_p, c_int, c_int]),
+    "ce_encode_image": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int]),
+    "ce_encode_text": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int]),
+    "ce_get_logits": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_int,
+                              c_void_p, c_void_p]),
+    "ce_cross_entropy": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "ce_pacl_project_patches": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int]),
+    "ce_pacl_project_text": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "ce_pacl_pool": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                             c_int, c_void_p, c_void_p]),
+    "ce_pacl_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                                c_void_p, c_void_p]),
+    "ce_sparc_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                 c_void_p, c_void_p, c_void_p]),
+    "ce_apply_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "ce_set_kernel_timing": (c_int, [c_void_p, c_int]),
+    "ce_kernel_stats": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_double), POINTER(c_int64),
+                                POINTER(c_double), POINTER(c_double)]),
+    "ce_kernel_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_int]),
+    "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
+    "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes library; raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libclipembed.so not found at {LIB_PATH}: build it with `make -C clip-embeds_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def check(status: int):
+    if status != CE_OK:
+        msg = lib().ce_last_error().decode(errors="replace")
+        raise ClipEmbedError(status, msg)
+
+
+def call(name: str, *args):
+    check(getattr(lib(), name)(*args))

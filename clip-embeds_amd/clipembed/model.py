@@ -1,0 +1,305 @@
+"""`clipembed.CLIP` — drop-in for the object returned by open_clip.create_model_and_transforms.
+
+Mirrors the surface the reference callers use:
+  encode_image / encode_text / get_logits / forward   open_clip/src/open_clip/model.py:279-310,415-435
+  model.visual.output_tokens (pacl.py:100), model.output_text_tokens (pacl.py:416, model.py:299-300)
+  logit_scale, state_dict() / load_state_dict(), .to(device), .eval(), .parameters()
+All compute runs in libclipembed (HIP, gfx950) through its C ABI; tensors cross the boundary
+as device pointers on the caller's current stream.  There is no CPU path: calling an encoder
+on a model that was never moved to a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import ModelConfig, get_model_config
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_TORCH_TO_CE = {torch.float32: _lib.CE_F32, torch.bfloat16: _lib.CE_BF16, torch.float16: _lib.CE_F16}
+
+
+class Engine:
+    """Owns one libclipembed handle on one device."""
+
+    def __init__(self, cfg: ModelConfig, device_index: int):
+        self.cfg = cfg
+        self.device = torch.device("cuda", device_index)
+        c = _lib.Config()
+        c.embed_dim = cfg.embed_dim
+        c.activation = _lib.CE_ACT_QUICK_GELU if cfg.quick_gelu else _lib.CE_ACT_GELU_ERF
+        c.image_size = cfg.vision.image_size
+        c.patch_size = cfg.vision.patch_size
+        c.vision = _lib.TowerConfig(cfg.vision.width, cfg.vision.layers, cfg.vision.heads, cfg.vision.mlp_width)
+        c.context_length = cfg.text.context_length
+        c.vocab_size = cfg.text.vocab_size
+        c.text = _lib.TowerConfig(cfg.text.width, cfg.text.layers, cfg.text.heads, cfg.text.mlp_width)
+        c.pacl_dim = cfg.pacl_dim
+        h = ctypes.c_void_p()
+        _lib.call("ce_create", ctypes.byref(c), device_index, ctypes.byref(h))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            _lib.lib().ce_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, sd: Dict[str, object], allow_unknown: bool = False):
+        keep = []
+        arr = (_lib.Tensor * max(1, len(sd)))()
+        for i, (k, v) in enumerate(sd.items()):
+            if isinstance(v, torch.Tensor):
+                v = v.detach().to("cpu")
+                if v.dtype == torch.bfloat16:
+                    a = v.contiguous().view(torch.int16).numpy()
+                    dt = _lib.CE_BF16
+                elif v.dtype == torch.float16:
+                    a = v.contiguous().view(torch.int16).numpy()
+                    dt = _lib.CE_F16
+                else:
+                    a = v.float().contiguous().numpy()
+                    dt = _lib.CE_F32
+            else:
+                a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+                dt = _lib.CE_F32
+            keep.append(a)
+            name = k.encode()
+            keep.append(name)
+            arr[i].name = name
+            arr[i].data = a.ctypes.data_as(ctypes.c_void_p)
+            arr[i].dtype = dt
+            arr[i].ndim = a.ndim
+            for d in range(min(4, a.ndim)):
+                arr[i].shape[d] = a.shape[d]
+        _lib.call("ce_load_weights", self.h, arr, len(sd), 1 if allow_unknown else 0)
+
+    def missing(self):
+        n = ctypes.c_int()
+        first = ctypes.c_char_p()
+        _lib.call("ce_missing_weights", self.h, ctypes.byref(n), ctypes.byref(first))
+        return n.value, (first.value or b"").decode()
+
+    # ---- timing (roofline reporting) ----
+    def set_timing(self, on: bool):
+        _lib.call("ce_set_kernel_timing", self.h, 1 if on else 0)
+
+    def kernel_stats(self):
+        out = []
+        i = 0
+        L = _lib.lib()
+        while True:
+            name = ctypes.create_string_buffer(64)
+            ms, n, fl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+            rc = L.ce_kernel_stats(self.h, i, name, 64, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
+                                   ctypes.byref(by))
+            if rc != _lib.CE_OK:
+                break
+            out.append({"name": name.value.decode(), "ms": ms.value, "launches": n.value, "flops": fl.value,
+                        "bytes": by.value})
+            i += 1
+        return out
+
+
+class VisualTower:
+    """Stands in for `model.visual` (attributes read or toggled by the reference callers)."""
+
+    def __init__(self, cfg: ModelConfig):
+        self.output_tokens = False
+        self.image_size = (cfg.vision.image_size, cfg.vision.image_size)
+        self.patch_size = (cfg.vision.patch_size, cfg.vision.patch_size)
+        self.grid_size = (cfg.vision.grid, cfg.vision.grid)
+        self.output_dim = cfg.embed_dim
+
+
+class CLIP(torch.nn.Module):
+    def __init__(self, cfg: ModelConfig, output_dict: bool = False):
+        super().__init__()
+        self.cfg = cfg
+        self.output_dict = output_dict
+        self.visual = VisualTower(cfg)
+        self.output_text_tokens = False
+        self.context_length = cfg.text.context_length
+        self.vocab_size = cfg.text.vocab_size
+        self.logit_scale = torch.nn.Parameter(torch.tensor(math.log(1 / 0.07)))
+        self.logit_bias = None
+        self._sd: Dict[str, torch.Tensor] = {}
+        self._engine: Optional[Engine] = None
+
+    # ---------------------------------------------------------------- weights / device
+    def load_state_dict(self, state_dict, strict: bool = True):
+        sd = {}
+        for k, v in state_dict.items():
+            t = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+            sd[k] = t.detach().cpu()
+        if "logit_scale" in sd:
+            with torch.no_grad():
+                self.logit_scale.copy_(sd["logit_scale"].reshape(()).float())
+        self._sd.update(sd)
+        if self._engine is not None:
+            self._engine.load(sd, allow_unknown=not strict)
+        return self
+
+    def state_dict(self, *args, **kwargs):
+        out = dict(self._sd)
+        out["logit_scale"] = self.logit_scale.detach().cpu().clone()
+        return out
+
+    def to(self, *args, **kwargs):
+        device = None
+        for a in list(args) + [kwargs.get("device")]:
+            if isinstance(a, (str, torch.device)):
+                device = torch.device(a)
+            elif isinstance(a, int):
+                device = torch.device("cuda", a)
+        super().to(*[a for a in args if not isinstance(a, (str, torch.device, int))],
+                    **{k: v for k, v in kwargs.items() if k != "device"})
+        if device is not None and device.type == "cuda":
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+            if self._engine is None or self._engine.device.index != idx:
+                self._engine = Engine(self.cfg, idx)
+                if self._sd:
+                    self._engine.load(self._sd)
+            self.logit_scale.data = self.logit_scale.data.to(device)
+        return self
+
+    def cuda(self, device=None):
+        return self.to(torch.device("cuda", device if device is not None else torch.cuda.current_device()))
+
+    @property
+    def engine(self) -> Engine:
+        if self._engine is None:
+            raise RuntimeError("clipembed runs only on a HIP device: call model.to('cuda') first")
+        return self._engine
+
+    @property
+    def device(self):
+        return self.engine.device
+
+    def _in(self, t: torch.Tensor, dtypes) -> torch.Tensor:
+        dev = self.engine.device
+        if t.device != dev:
+            t = t.to(dev)
+        if t.dtype not in dtypes:
+            t = t.to(dtypes[0])
+        return t.contiguous()
+
+    # ---------------------------------------------------------------- encoders
+    @torch.no_grad()
+    def encode_image(self, image: torch.Tensor, normalize: bool = False):
+        e = self.engine
+        image = self._in(image, (torch.float32, torch.bfloat16))
+        v = self.cfg.vision
+        if image.dim() != 4 or tuple(image.shape[1:]) != (3, v.image_size, v.image_size):
+            raise RuntimeError(f"encode_image expects [B,3,{v.image_size},{v.image_size}], got {tuple(image.shape)}")
+        B = image.shape[0]
+        pooled = torch.empty(B, self.cfg.embed_dim, device=e.device, dtype=torch.float32)
+        tokens = None
+        if self.visual.output_tokens:
+            tokens = torch.empty(B, v.num_patches, v.width, device=e.device, dtype=torch.float32)
+        _lib.call("ce_encode_image", e.h, _stream(e.device), _ptr(image), _TORCH_TO_CE[image.dtype], B,
+                  1 if normalize else 0, _ptr(pooled), _ptr(tokens), _lib.CE_F32)
+        return (pooled, tokens) if self.visual.output_tokens else pooled
+
+    @torch.no_grad()
+    def encode_text(self, text: torch.Tensor, normalize: bool = False):
+        e = self.engine
+        text = self._in(text, (torch.int64,))
+        t = self.cfg.text
+        if text.dim() != 2 or text.shape[1] != t.context_length:
+            raise RuntimeError(f"encode_text expects [B,{t.context_length}] token ids, got {tuple(text.shape)}")
+        B = text.shape[0]
+        pooled = torch.empty(B, self.cfg.embed_dim, device=e.device, dtype=torch.float32)
+        tokens = None
+        if self.output_text_tokens:
+            tokens = torch.empty(B, t.context_length, t.width, device=e.device, dtype=torch.float32)
+        _lib.call("ce_encode_text", e.h, _stream(e.device), _ptr(text), B, t.context_length,
+                  1 if normalize else 0, _ptr(pooled), _ptr(tokens), _lib.CE_F32)
+        return (pooled, tokens) if self.output_text_tokens else pooled
+
+    @torch.no_grad()
+    def logits(self, image_features: torch.Tensor, text_features: torch.Tensor, scale: float,
+               normalize: bool = False, with_text_logits: bool = True):
+        """scale * I @ T^T (+ its transpose) in one fused kernel (model.py:306-309)."""
+        e = self.engine
+        a = self._in(image_features, (torch.float32,))
+        b = self._in(text_features, (torch.float32,))
+        Bi, D = a.shape
+        Bt = b.shape[0]
+        il = torch.empty(Bi, Bt, device=e.device, dtype=torch.float32)
+        tl = torch.empty(Bt, Bi, device=e.device, dtype=torch.float32) if with_text_logits else None
+        _lib.call("ce_get_logits", e.h, _stream(e.device), _ptr(a), Bi, _ptr(b), Bt, D, float(scale),
+                  1 if normalize else 0, _ptr(il), _ptr(tl))
+        return il, tl
+
+    def get_logits(self, image, text):
+        image_features = self._pooled(self.encode_image(image, normalize=True))
+        text_features = self._pooled(self.encode_text(text, normalize=True))
+        return self.logits(image_features, text_features, float(self.logit_scale.exp()))
+
+    @staticmethod
+    def _pooled(x):
+        return x[0] if isinstance(x, tuple) else x
+
+    def forward(self, image: Optional[torch.Tensor] = None, text: Optional[torch.Tensor] = None):
+        image_features = self._pooled(self.encode_image(image, normalize=True)) if image is not None else None
+        text_features = self._pooled(self.encode_text(text, normalize=True)) if text is not None else None
+        if self.output_dict:
+            return {"image_features": image_features, "text_features": text_features,
+                    "logit_scale": self.logit_scale.exp()}
+        return image_features, text_features, self.logit_scale.exp()
+
+
+def create_model(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = None, device=None,
+                 state_dict: Optional[dict] = None, output_dict: bool = False, **_ignored) -> CLIP:
+    """open_clip.create_model equivalent (factory.py:241-613) for the registered CLIP configs.
+
+    pretrained: None (weights must then be supplied via `state_dict`/load_state_dict) or a path
+    to a local open_clip state dict (.pt/.bin loaded with weights_only=True, or .safetensors).
+    """
+    cfg = get_model_config(model_name)
+    model = CLIP(cfg, output_dict=output_dict)
+    if pretrained:
+        model.load_state_dict(load_checkpoint_file(pretrained))
+    if state_dict is not None:
+        model.load_state_dict(state_dict)
+    if device is not None:
+        model.to(device)
+    return model
+
+
+def create_model_and_transforms(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = None,
+                                device=None, **kw):
+    """Returns (model, preprocess_train, preprocess_val) like open_clip (factory.py:822-958).
+    Image preprocessing is outside the drop-in boundary ('next'): both transforms are
+    None; callers feed normalised [B,3,336,336] tensors."""
+    return create_model(model_name, pretrained, device, **kw), None, None
+
+
+def load_checkpoint_file(path: str) -> dict:
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(path)
+    else:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "state_dict" in sd:
+            sd = sd["state_dict"]
+    return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}

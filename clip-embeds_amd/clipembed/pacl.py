@@ -1,0 +1,195 @@
+"""PACL / SPARC heads on top of the engine — mirrors Patch-Aligned-Contrastive-Learning/model/pacl.py.
+
+Class names and forward signatures follow the reference so eval drivers read the same:
+  open_clip_pacl            pacl.py:51-145  (forward: ones-weighted patch sum, "Eval only" overwrite :142)
+  open_clip_pacl_rope       pacl.py:184-197 (RoPE on the 1024-d patch tokens before the head)
+  open_clip_pacl_rope_after pacl.py:199-209 (RoPE on projected tokens, sigmoid(10 cos) weights)
+  sparc                     pacl.py:380-478 (forward / scoring / forward_text mask)
+  apply_rope                pacl.py:147-181
+Everything runs through libclipembed; the fused pooling is ce_pacl_pool.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .config import get_model_config
+from .model import CLIP, _ptr, _stream
+from .weights import synthetic_pacl_heads
+
+
+class open_clip_pacl(torch.nn.Module):
+    weight_mode = _lib.CE_PACL_ONES
+    rope = _lib.CE_ROPE_NONE
+
+    def __init__(self, base_model: str = "ViT-L-14-336", clip_state_dict=None, device=None, cfg=None):
+        super().__init__()
+        if cfg is None:
+            if base_model != "ViT-L-14-336":
+                raise NotImplementedError(f"clipembed implements the ViT-L-14-336 PACL head only, not {base_model}")
+            cfg = get_model_config(base_model)
+        cfg = cfg.with_pacl(768)
+        self.clip_model = CLIP(cfg)
+        self.clip_model.visual.output_tokens = True          # pacl.py:100
+        if clip_state_dict is not None:
+            self.clip_model.load_state_dict(clip_state_dict)
+        self._heads = {}
+        if device is not None:
+            self.to(device)
+
+    # state dict with the reference's key layout: clip_model.* + visual_projection.* + text_projection.*
+    def load_state_dict(self, sd, strict: bool = True):
+        clip, heads = {}, {}
+        for k, v in sd.items():
+            k2 = k[7:] if k.startswith("module.") else k        # eval_pacl.py:380-388
+            if k2.startswith("clip_model."):
+                clip[k2[len("clip_model."):]] = v
+            else:
+                heads[k2] = v
+        if clip:
+            self.clip_model.load_state_dict(clip, strict=strict)
+        if heads:
+            self._heads.update(heads)
+            if self.clip_model._engine is not None:
+                self.clip_model._engine.load(heads, allow_unknown=not strict)
+        return self
+
+    def init_synthetic_heads(self, seed: int = 11):
+        return self.load_state_dict(synthetic_pacl_heads(self.clip_model.cfg, seed))
+
+    def to(self, *args, **kwargs):
+        self.clip_model.to(*args, **kwargs)
+        if self._heads and self.clip_model._engine is not None:
+            self.clip_model._engine.load(self._heads, allow_unknown=True)
+        return self
+
+    @property
+    def engine(self):
+        return self.clip_model.engine
+
+    @torch.no_grad()
+    def forward_visual(self, images):
+        """visual_projection(encode_image tokens) -> [B, 576, 768] (pacl.py:112-114)."""
+        e = self.engine
+        _, tokens = self.clip_model.encode_image(images)
+        if self.rope == _lib.CE_ROPE_BEFORE:
+            tokens = apply_rope(tokens, engine=e)
+        B, P, _ = tokens.shape
+        out = torch.empty(B, P, self.clip_model.cfg.pacl_dim, device=e.device, dtype=torch.float32)
+        _lib.call("ce_pacl_project_patches", e.h, _stream(e.device), _ptr(tokens), _lib.CE_F32, B, P,
+                  _lib.CE_ROPE_NONE, _ptr(out), _lib.CE_F32)
+        return out
+
+    @torch.no_grad()
+    def forward_text(self, caps):
+        """text_projection(encode_text) -> [B, 768] (pacl.py:116-118)."""
+        e = self.engine
+        t = self.clip_model.encode_text(caps)
+        out = torch.empty(t.shape[0], self.clip_model.cfg.pacl_dim, device=e.device, dtype=torch.float32)
+        _lib.call("ce_pacl_project_text", e.h, _stream(e.device), _ptr(t), t.shape[0], _ptr(out))
+        return out
+
+    @torch.no_grad()
+    def pool(self, visual_proj, text_proj):
+        """Fused patch alignment + weighted patch sum + L2 norms (pacl.py:120-145)."""
+        e = self.engine
+        vp = visual_proj.contiguous()
+        tp = text_proj.float().contiguous()
+        Bi, P, D = vp.shape
+        Bt = tp.shape[0]
+        R = max(Bi, Bt)
+        oi = torch.empty(R, D, device=e.device, dtype=torch.float32)
+        ot = torch.empty(Bt, D, device=e.device, dtype=torch.float32)
+        dt = _lib.CE_BF16 if vp.dtype == torch.bfloat16 else _lib.CE_F32
+        _lib.call("ce_pacl_pool", e.h, _stream(e.device), _ptr(vp), dt, Bi, P, _ptr(tp), Bt, D,
+                  self.weight_mode, 1 if self.rope == _lib.CE_ROPE_AFTER else 0, _ptr(oi), _ptr(ot))
+        return oi, ot
+
+    @torch.no_grad()
+    def forward(self, images, caps):
+        """Whole PACL forward in one engine call (pacl.py:135-145 and the rope variants)."""
+        e = self.engine
+        images = self.clip_model._in(images, (torch.float32, torch.bfloat16))
+        caps = self.clip_model._in(caps, (torch.int64,))
+        Bi, Bt = images.shape[0], caps.shape[0]
+        D = self.clip_model.cfg.pacl_dim
+        oi = torch.empty(max(Bi, Bt), D, device=e.device, dtype=torch.float32)
+        ot = torch.empty(Bt, D, device=e.device, dtype=torch.float32)
+        pdt = _lib.CE_BF16 if images.dtype == torch.bfloat16 else _lib.CE_F32
+        _lib.call("ce_pacl_forward", e.h, _stream(e.device), _ptr(images), pdt, Bi, _ptr(caps), Bt,
+                  self.weight_mode, self.rope, _ptr(oi), _ptr(ot))
+        return oi, ot
+
+
+class open_clip_pacl_rope(open_clip_pacl):
+    rope = _lib.CE_ROPE_BEFORE
+
+
+class open_clip_pacl_rope_after(open_clip_pacl):
+    weight_mode = _lib.CE_PACL_SIGMOID10
+    rope = _lib.CE_ROPE_AFTER
+
+
+class open_clip_pacl_sigmoid(open_clip_pacl):
+    """sigmoid(10 cos) weighting without RoPE (the reference's *_base weighting, pacl.py:362-363)."""
+    weight_mode = _lib.CE_PACL_SIGMOID10
+
+
+@torch.no_grad()
+def apply_rope(embeddings: torch.Tensor, engine=None) -> torch.Tensor:
+    """apply_rope (pacl.py:147-181) on device; positions 0..P-1, de-interleaved output."""
+    if engine is None:
+        raise RuntimeError("apply_rope needs an engine (its RoPE tables live on the device)")
+    x = embeddings.float().contiguous()
+    B, P, D = x.shape
+    out = torch.empty_like(x)
+    _lib.call("ce_apply_rope", engine.h, _stream(engine.device), _ptr(x), B, P, D, _ptr(out))
+    return out
+
+
+class sparc(open_clip_pacl):
+    """SPARC (pacl.py:380-478) on the ViT-L-14-336 head."""
+
+    def __init__(self, sigma: float = 1.0 / 625, base_model: str = "ViT-L-14-336", **kw):
+        super().__init__(base_model, **kw)
+        self.sigma = sigma
+        self.clip_model.output_text_tokens = True            # pacl.py:416
+
+    @torch.no_grad()
+    def forward_text(self, caps):
+        e = self.engine
+        caps = self.clip_model._in(caps, (torch.int64,))
+        _, tokens = self.clip_model.encode_text(caps)
+        B, T, Dt = tokens.shape
+        D = self.clip_model.cfg.pacl_dim
+        out = torch.empty(B, T, D, device=e.device, dtype=torch.float32)
+        _lib.call("ce_pacl_project_text", e.h, _stream(e.device), _ptr(tokens), B * T, _ptr(out))
+        eots = caps.argmax(dim=-1)
+        mask = (torch.arange(T, device=caps.device).expand(B, -1) <= eots.unsqueeze(1)).float()
+        return out, mask
+
+    @torch.no_grad()
+    def forward(self, images, caps):
+        e = self.engine
+        v = self.forward_visual(images)
+        l, mask = self.forward_text(caps)
+        B, P, D = v.shape
+        T = l.shape[1]
+        grouped = torch.empty(B, T, D, device=e.device, dtype=torch.float32)
+        l_norm = torch.empty_like(grouped)
+        _lib.call("ce_sparc_forward", e.h, _stream(e.device), _ptr(v), _ptr(l), B, P, T, D, float(self.sigma),
+                  _ptr(grouped), _ptr(l_norm), None)
+        return v, l_norm, grouped, mask
+
+    @torch.no_grad()
+    def scoring(self, images, caps, local: bool = False):
+        if images.shape[0] == 1 and caps.shape[0] > 1:
+            images = images.expand(caps.shape[0], *images.shape[1:])
+        assert images.shape[0] == caps.shape[0]
+        v, l, g, _ = self.forward(images, caps)
+        gt = torch.nn.functional.normalize(l.mean(dim=1), dim=-1)
+        if not local:
+            gi = torch.nn.functional.normalize(v.mean(dim=1), dim=-1)
+        else:
+            gi = torch.nn.functional.normalize(g.mean(dim=1), dim=-1)
+        return self.clip_model.logits(gi, gt, 1.0, with_text_logits=False)[0]

@@ -1,0 +1,222 @@
+// Fused multi-head attention forward (flash-style, online softmax) for gfx950.
+//
+// Replaces the nn.MultiheadAttention core inside ResidualAttentionBlock.attention
+// (open_clip/src/open_clip/transformer.py:242-255): softmax(q k^T / sqrt(64) + mask) v per head,
+// with the additive causal -inf mask of the text tower (transformer.py:960-966).
+//
+// Layout: qkv [B*L][3D] bf16 as produced by the in_proj GEMM (q | k | v, head h at columns
+// h*64..h*64+63 of each third, nn.MultiheadAttention packing); out [B*L][D] bf16.
+//
+// Design:
+//  * workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32 queries.
+//  * K/V tiles of 64 keys staged global->LDS with global_load_lds_dwordx4 into a 2-deep ring
+//    (next tile issued before the current one is consumed, counted vmcnt).
+//  * "Swapped" QK^T: S^T = K Q^T with v_mfma_f32_32x32x16_bf16 so each lane holds one query
+//    (lane&31) and 32 of the tile's keys in registers — the row max/sum are in-lane plus one
+//    cross-half exchange (lanes l, l^32).
+//  * P stays in registers: the S^T accumulator, packed to bf16, is directly the B operand of
+//    O^T = V^T P^T (no LDS round trip); V^T fragments come from ds_read_b64_tr_b16 on the
+//    row-major V tile.  O^T keeps the query on the lane, so the online-softmax rescale is a
+//    per-lane scalar.
+//  * K tile LDS image swizzled (16-B chunk c of row r at c ^ ((r>>1)&7)) for conflict-free
+//    ds_read_b128; ragged tails (L = 577 = 9*64 + 1, L = 77) are clamped on load and masked
+//    with -inf in the scores.
+#include "ce_device.h"
+#include "ce_kernels.h"
+
+namespace ce {
+namespace {
+
+constexpr int QBLK = 128;
+constexpr int KBLK = 64;
+constexpr int TILE_KV_BYTES = KBLK * 64 * 2;       // 8 KB per K or V tile
+constexpr int STAGE_BYTES = 2 * TILE_KV_BYTES;      // K + V
+
+__device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((CE_LDS s16x4*)(p));
+}
+
+__device__ __forceinline__ void barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
+                                                    bf16_t* __restrict__ out, int L, int H,
+                                                    float scale_log2) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+
+    const int b = blockIdx.z, h = blockIdx.y, qb = blockIdx.x;
+    const int D = H * 64;
+    const long ld = 3L * D;
+    const bf16_t* base = qkv + (size_t)b * L * ld;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h2 = lane >> 5;
+    const int qrow = qb * QBLK + wave * 32 + r;
+
+    // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
+    bf16x8 qf[4];
+    {
+        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+    }
+
+    // staging: thread -> row tid>>3 of a 32-row pass, 16-B chunk tid&7
+    const int srow = tid >> 3;
+    const int spos = tid & 7;
+    const int kchunk = spos ^ ((tid >> 4) & 7);
+    const int kv_end = CAUSAL ? min(L, qb * QBLK + QBLK) : L;
+    const int nkt = (kv_end + KBLK - 1) / KBLK;
+    const bf16_t* kbase = base + D + h * 64;
+    const bf16_t* vbase = base + 2 * D + h * 64;
+
+    auto stage = [&](int t, int buf) {
+        char* dst = smem + buf * STAGE_BYTES + wave * 1024;
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            const int key = min(t * KBLK + ps * 32 + srow, L - 1);
+            glds16(kbase + (size_t)key * ld + kchunk * 8, dst + ps * 4096);
+            glds16(vbase + (size_t)key * ld + spos * 8, dst + TILE_KV_BYTES + ps * 4096);
+        }
+    };
+
+    // per-lane LDS read offsets
+    int koff[2][4];
+#pragma unroll
+    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int row = kt2 * 32 + r;
+            koff[kt2][ks] = row * 128 + (((2 * ks + h2) ^ ((row >> 1) & 7)) << 4);
+        }
+    // V^T via ds_read_b64_tr_b16: 16-lane group G supplies rows (keys) kb + 4*(G>>1) + (i>>2),
+    // columns dt*32 + 16*(G&1) + 4*(i&3)
+    const int G = lane >> 4, gi = lane & 15;
+    const int voff_lane = (4 * (G >> 1) + (gi >> 2)) * 128 + (16 * (G & 1) + 4 * (gi & 3)) * 2;
+
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+    float m_run = -INFINITY;
+    float l_run = 0.f;   // partial (this half's keys)
+
+    stage(0, 0);
+    for (int t = 0; t < nkt; ++t) {
+        if (t + 1 < nkt) {
+            stage(t + 1, (t + 1) & 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();
+        const char* kb = smem + (t & 1) * STAGE_BYTES;
+        const char* vb = kb + TILE_KV_BYTES;
+
+        // ---- S^T = K Q^T (two 32-key subtiles) ----
+        f32x16 s[2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
+            }
+        }
+
+        // ---- online softmax (log2 domain) ----
+        const int key0 = t * KBLK;
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
+                float x = s[kt2][i] * scale_log2;
+                const bool masked = (key >= L) || (CAUSAL && key > qrow);
+                x = masked ? -INFINITY : x;
+                s[kt2][i] = x;
+                tmax = fmaxf(tmax, x);
+            }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = exp2f(m_run - m_new);
+        m_run = m_new;
+        float psum = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = exp2f(s[kt2][8 * s2 + j] - m_new);
+                    psum += pv;
+                    pf[kt2][s2][j] = (__bf16)pv;
+                }
+        l_run = l_run * alpha + psum;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+
+        // ---- O^T += V^T P^T ----
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int krow = kt2 * 32 + 16 * s2;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    const char* a0 = vb + krow * 128 + dt * 64 + voff_lane;
+                    const s16x4 lo = ds_read_tr16(a0);
+                    const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
+                    typedef __attribute__((ext_vector_type(8))) short s16x8;
+                    const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
+                }
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+    }
+
+    // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.0f / l_tot;
+    if (qrow < L) {
+        bf16_t* op = out + ((size_t)b * L + qrow) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d0 = dt * 32 + 8 * g + 4 * h2;
+                uint2 w;
+                w.x = pack_bf2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+                w.y = pack_bf2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+                *reinterpret_cast<uint2*>(op + d0) = w;
+            }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal,
+                            hipStream_t s) {
+    if (B <= 0 || L <= 0) return hipSuccess;
+    const dim3 grid((L + QBLK - 1) / QBLK, H, B);
+    const float scale_log2 = 0.125f * 1.4426950408889634f;   // 1/sqrt(64) * log2(e)
+    if (causal)
+        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, scale_log2);
+    else
+        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, scale_log2);
+    return hipGetLastError();
+}
+
+}  // namespace ce

@@ -1,0 +1,1055 @@
+// C ABI of libclipembed (include/clipembed.h): weight registry, workspace, tower orchestration.
+//
+// The tower forward mirrors open_clip (reference paths relative to the reference root):
+//   VisionTransformer.forward   open_clip/src/open_clip/transformer.py:825-836
+//     _embeds :701-716  (conv1 -> +cls -> +pos -> ln_pre)
+//     24 x ResidualAttentionBlock.forward :257-268  (x += attn(ln_1 x); x += mlp(ln_2 x))
+//     _pool :718-741 ('tok': ln_post on all tokens, pooled = row 0), pooled @ proj
+//   CLIP.encode_text            open_clip/src/open_clip/model.py:283-301
+//   CLIP.get_logits             model.py:303-310
+// The residual stream is kept in f32 in HBM; every GEMM reads bf16 activations and bf16
+// weights and accumulates in f32 (MFMA); LayerNorm statistics are f32.
+#include "../../include/clipembed.h"
+#include "ce_kernels.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+using ce::bf16_t;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(CE_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),         \
+                        __FILE__, __LINE__);                                                      \
+    } while (0)
+
+#define CE_TRY(expr)                     \
+    do {                                 \
+        int rc_ = (expr);                \
+        if (rc_ != CE_OK) return rc_;    \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+enum Store { ST_F32, ST_BF16, ST_BF16_PADK, ST_F32_T, ST_SCALAR };
+
+struct WSpec {
+    std::vector<int64_t> shape;
+    Store st;
+    bool required;   // required for the CLIP towers
+};
+
+inline uint16_t host_f2bf(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+inline float host_bf2f(uint16_t v) {
+    uint32_t u = (uint32_t)v << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+inline float host_h2f(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000) << 16;
+    uint32_t exp = (h >> 10) & 0x1f, man = h & 0x3ff, u;
+    if (exp == 0) {
+        if (man == 0) u = sign;
+        else {
+            exp = 127 - 15 + 1;
+            while (!(man & 0x400)) { man <<= 1; --exp; }
+            man &= 0x3ff;
+            u = sign | (exp << 23) | (man << 13);
+        }
+    } else if (exp == 31) {
+        u = sign | 0x7f800000u | (man << 13);
+    } else {
+        u = sign | ((exp + 127 - 15) << 23) | (man << 13);
+    }
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+struct Blk {
+    const float *ln1w, *ln1b, *bqkv, *bout, *ln2w, *ln2b, *bfc, *bproj;
+    const bf16_t *wqkv, *wout, *wfc, *wproj;
+};
+
+struct KStat {
+    std::string name;
+    double ms = 0, flops = 0, bytes = 0;
+    int64_t n = 0;
+};
+struct Pending {
+    int tag;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct ce_handle {
+    ce_config cfg{};
+    int device = 0;
+    std::map<std::string, WSpec> specs;
+    std::map<std::string, std::string> alias;
+    std::map<std::string, void*> dptr;
+    std::map<std::string, bool> loaded;
+    float logit_scale = std::log(1.0f / 0.07f);
+    int Kp = 0;      // padded patch K
+    int G = 0;       // patch grid side
+    // workspace
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    char* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    float* scratch = nullptr;    // 256 B
+    // RoPE tables (pacl.py:147-181): [P][D/2] for D = vision width and D = pacl_dim
+    float *rc_v = nullptr, *rs_v = nullptr, *rc_p = nullptr, *rs_p = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<KStat> stats;
+    std::map<std::string, int> stat_idx;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_ev;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// weight registry
+void add_block_specs(ce_handle* h, const std::string& p, int D, int F) {
+    auto& s = h->specs;
+    s[p + "ln_1.weight"] = {{D}, ST_F32, true};
+    s[p + "ln_1.bias"] = {{D}, ST_F32, true};
+    s[p + "attn.in_proj_weight"] = {{3 * D, D}, ST_BF16, true};
+    s[p + "attn.in_proj_bias"] = {{3 * D}, ST_F32, true};
+    s[p + "attn.out_proj.weight"] = {{D, D}, ST_BF16, true};
+    s[p + "attn.out_proj.bias"] = {{D}, ST_F32, true};
+    s[p + "ln_2.weight"] = {{D}, ST_F32, true};
+    s[p + "ln_2.bias"] = {{D}, ST_F32, true};
+    s[p + "mlp.c_fc.weight"] = {{F, D}, ST_BF16, true};
+    s[p + "mlp.c_fc.bias"] = {{F}, ST_F32, true};
+    s[p + "mlp.c_proj.weight"] = {{D, F}, ST_BF16, true};
+    s[p + "mlp.c_proj.bias"] = {{D}, ST_F32, true};
+}
+
+void build_specs(ce_handle* h) {
+    const ce_config& c = h->cfg;
+    auto& s = h->specs;
+    const int Dv = c.vision.width, Dt = c.text.width, E = c.embed_dim;
+    const int Lv = h->G * h->G + 1;
+    s["visual.class_embedding"] = {{Dv}, ST_F32, true};
+    s["visual.positional_embedding"] = {{Lv, Dv}, ST_F32, true};
+    s["visual.proj"] = {{Dv, E}, ST_F32, true};
+    s["visual.conv1.weight"] = {{Dv, 3, c.patch_size, c.patch_size}, ST_BF16_PADK, true};
+    s["visual.ln_pre.weight"] = {{Dv}, ST_F32, true};
+    s["visual.ln_pre.bias"] = {{Dv}, ST_F32, true};
+    s["visual.ln_post.weight"] = {{Dv}, ST_F32, true};
+    s["visual.ln_post.bias"] = {{Dv}, ST_F32, true};
+    for (int i = 0; i < c.vision.layers; ++i)
+        add_block_specs(h, "visual.transformer.resblocks." + std::to_string(i) + ".", Dv, c.vision.mlp_width);
+    s["token_embedding.weight"] = {{c.vocab_size, Dt}, ST_F32, true};
+    s["positional_embedding"] = {{c.context_length, Dt}, ST_F32, true};
+    s["text_projection"] = {{Dt, E}, ST_F32, true};
+    s["ln_final.weight"] = {{Dt}, ST_F32, true};
+    s["ln_final.bias"] = {{Dt}, ST_F32, true};
+    for (int i = 0; i < c.text.layers; ++i)
+        add_block_specs(h, "transformer.resblocks." + std::to_string(i) + ".", Dt, c.text.mlp_width);
+    s["logit_scale"] = {{}, ST_SCALAR, false};
+    if (c.pacl_dim > 0) {
+        const int Pd = c.pacl_dim;
+        // open_clip_pacl heads, pacl.py:70-79 (Sequential(LayerNorm, Dropout, Patch_Projection))
+        s["visual_projection.0.weight"] = {{Dv}, ST_F32, false};
+        s["visual_projection.0.bias"] = {{Dv}, ST_F32, false};
+        s["visual_projection.2.linear_projection.0.weight"] = {{Pd, Dv}, ST_BF16, false};
+        s["visual_projection.2.linear_projection.0.bias"] = {{Pd}, ST_F32, false};
+        s["visual_projection.2.non_linear_projection.0.weight"] = {{Pd, Dv}, ST_BF16, false};
+        s["visual_projection.2.non_linear_projection.0.bias"] = {{Pd}, ST_F32, false};
+        s["visual_projection.2.non_linear_projection.2.weight"] = {{Pd, Pd}, ST_BF16, false};
+        s["visual_projection.2.non_linear_projection.2.bias"] = {{Pd}, ST_F32, false};
+        s["text_projection.0.weight"] = {{E}, ST_F32, false};
+        s["text_projection.0.bias"] = {{E}, ST_F32, false};
+        s["text_projection.2.weight"] = {{Pd, E}, ST_F32_T, false};
+        s["text_projection.2.bias"] = {{Pd}, ST_F32, false};
+        // Patch_Projection registers the same Sequential twice (pacl.py:39)
+        h->alias["visual_projection.2.text_projection.0.weight"] = "visual_projection.2.linear_projection.0.weight";
+        h->alias["visual_projection.2.text_projection.0.bias"] = "visual_projection.2.linear_projection.0.bias";
+    }
+}
+
+std::string canonical(const ce_handle* h, const char* raw) {
+    std::string n(raw);
+    for (;;) {
+        if (n.rfind("module.", 0) == 0) n = n.substr(7);
+        else if (n.rfind("clip_model.", 0) == 0) n = n.substr(11);
+        else break;
+    }
+    auto it = h->alias.find(n);
+    if (it != h->alias.end()) return it->second;
+    return n;
+}
+
+template <class T = float>
+const T* W(const ce_handle* h, const std::string& n) {
+    auto it = h->dptr.find(n);
+    return it == h->dptr.end() ? nullptr : static_cast<const T*>(it->second);
+}
+
+Blk block_ptrs(const ce_handle* h, const std::string& p) {
+    Blk b;
+    b.ln1w = W(h, p + "ln_1.weight");
+    b.ln1b = W(h, p + "ln_1.bias");
+    b.bqkv = W(h, p + "attn.in_proj_bias");
+    b.bout = W(h, p + "attn.out_proj.bias");
+    b.ln2w = W(h, p + "ln_2.weight");
+    b.ln2b = W(h, p + "ln_2.bias");
+    b.bfc = W(h, p + "mlp.c_fc.bias");
+    b.bproj = W(h, p + "mlp.c_proj.bias");
+    b.wqkv = W<bf16_t>(h, p + "attn.in_proj_weight");
+    b.wout = W<bf16_t>(h, p + "attn.out_proj.weight");
+    b.wfc = W<bf16_t>(h, p + "mlp.c_fc.weight");
+    b.wproj = W<bf16_t>(h, p + "mlp.c_proj.weight");
+    return b;
+}
+
+int check_ready(ce_handle* h, bool need_pacl) {
+    for (auto& kv : h->specs) {
+        const bool pacl = kv.first.rfind("visual_projection.", 0) == 0 || kv.first.rfind("text_projection.", 0) == 0;
+        if ((kv.second.required || (need_pacl && pacl)) && !h->loaded[kv.first])
+            return fail(CE_ERR_STATE, "weight '%s' has not been loaded", kv.first.c_str());
+    }
+    return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// timing
+int stat_tag(ce_handle* h, const char* name) {
+    auto it = h->stat_idx.find(name);
+    if (it != h->stat_idx.end()) return it->second;
+    const int idx = (int)h->stats.size();
+    h->stats.push_back(KStat{name});
+    h->stat_idx[name] = idx;
+    return idx;
+}
+
+hipEvent_t get_event(ce_handle* h) {
+    if (!h->free_ev.empty()) {
+        hipEvent_t e = h->free_ev.back();
+        h->free_ev.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+template <class F>
+int timed(ce_handle* h, hipStream_t s, const char* name, double flops, double bytes, F&& launch) {
+    if (!h->timing) {
+        hipError_t e = launch();
+        if (e != hipSuccess) return fail(CE_ERR_HIP, "%s launch failed: %s", name, hipGetErrorString(e));
+        return CE_OK;
+    }
+    const int tag = stat_tag(h, name);
+    hipEvent_t a = get_event(h), b = get_event(h);
+    (void)hipEventRecord(a, s);
+    hipError_t e = launch();
+    (void)hipEventRecord(b, s);
+    if (e != hipSuccess) return fail(CE_ERR_HIP, "%s launch failed: %s", name, hipGetErrorString(e));
+    h->pending.push_back({tag, a, b});
+    h->stats[tag].flops += flops;
+    h->stats[tag].bytes += bytes;
+    h->stats[tag].n += 1;
+    return CE_OK;
+}
+
+int resolve_pending(ce_handle* h) {
+    for (auto& p : h->pending) {
+        HIP_TRY(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+        h->stats[p.tag].ms += ms;
+        h->free_ev.push_back(p.a);
+        h->free_ev.push_back(p.b);
+    }
+    h->pending.clear();
+    return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// workspace
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct TowerWs {
+    float* x;
+    bf16_t *xn, *qkv, *att, *hid;
+    float* pooled;
+    int* rows;
+};
+
+size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
+    size_t n = 0;
+    n += align256(rows * D * 4);
+    n += align256(rows * D * 2);
+    n += align256(rows * 3 * D * 2);
+    n += align256(rows * D * 2);
+    n += align256(std::max(rows * F, extra_hid_elems) * 2);
+    n += align256(B * D * 4);
+    n += align256(B * 4);
+    return n;
+}
+
+TowerWs carve(char* base, long rows, int D, int F, long extra_hid_elems, long B) {
+    TowerWs w;
+    char* p = base;
+    w.x = (float*)p; p += align256(rows * D * 4);
+    w.xn = (bf16_t*)p; p += align256(rows * D * 2);
+    w.qkv = (bf16_t*)p; p += align256(rows * 3 * D * 2);
+    w.att = (bf16_t*)p; p += align256(rows * D * 2);
+    w.hid = (bf16_t*)p; p += align256(std::max(rows * F, extra_hid_elems) * 2);
+    w.pooled = (float*)p; p += align256(B * D * 4);
+    w.rows = (int*)p;
+    return w;
+}
+
+size_t vision_bytes(const ce_handle* h, long B) {
+    const long Lv = (long)h->G * h->G + 1;
+    return tower_bytes(B * Lv, h->cfg.vision.width, h->cfg.vision.mlp_width, B * h->G * h->G * h->Kp, B);
+}
+size_t text_bytes(const ce_handle* h, long B) {
+    return tower_bytes(B * h->cfg.context_length, h->cfg.text.width, h->cfg.text.mlp_width, 0, B);
+}
+
+int ensure_ws(ce_handle* h, size_t need) {
+    if (need <= h->ws_bytes) return CE_OK;
+    HIP_TRY(hipDeviceSynchronize());
+    if (h->ws) HIP_TRY(hipFree(h->ws));
+    h->ws = nullptr;
+    h->ws_bytes = 0;
+    if (hipMalloc(&h->ws, need) != hipSuccess) {
+        h->ws = nullptr;
+        (void)hipGetLastError();
+        return fail(CE_ERR_OOM, "cannot allocate %zu bytes of workspace", need);
+    }
+    h->ws_bytes = need;
+    return CE_OK;
+}
+
+int ensure_tmp(ce_handle* h, size_t need) {
+    if (need <= h->tmp_bytes) return CE_OK;
+    HIP_TRY(hipDeviceSynchronize());
+    if (h->tmp) HIP_TRY(hipFree(h->tmp));
+    h->tmp = nullptr;
+    h->tmp_bytes = 0;
+    if (hipMalloc(&h->tmp, need) != hipSuccess) {
+        h->tmp = nullptr;
+        (void)hipGetLastError();
+        return fail(CE_ERR_OOM, "cannot allocate %zu bytes of scratch", need);
+    }
+    h->tmp_bytes = need;
+    return CE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// building blocks
+int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
+         int M, int N, int K, const float* bias, int act, const float* resid, void* out, bool out_bf16,
+         int grp = 0, int o_gs = 0, int o_go = 0, int r_gs = 0, int r_go = 0) {
+    ce::GemmParams p{};
+    p.A = A; p.lda = lda; p.W = Wt; p.ldw = K;
+    p.M = M; p.N = N; p.K = K;
+    p.bias = bias;
+    p.resid = resid; p.ldr = N;
+    p.out = out; p.ldo = N;
+    p.grp = grp; p.o_gs = o_gs; p.o_go = o_go; p.r_gs = r_gs; p.r_go = r_go;
+    const double flops = 2.0 * M * N * K;
+    const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
+                         (resid ? (double)M * N * 4 : 0.0);
+    return timed(h, s, tag, flops, bytes, [&] { return ce::launch_gemm(p, act, out_bf16, s); });
+}
+
+int layernorm(ce_handle* h, hipStream_t s, const char* tag, const float* in, void* out, bool out_bf16,
+              const float* w, const float* b, int rows, int D, int grp = 0, int i_gs = 0, int i_go = 0,
+              int o_gs = 0, int o_go = 0, const float* w2 = nullptr, const float* b2 = nullptr,
+              const float* rc = nullptr, const float* rs = nullptr, int rope_P = 1) {
+    ce::LNParams p{};
+    p.in = in; p.ldi = D; p.out = out; p.ldo = D;
+    p.w = w; p.b = b; p.rows = rows; p.D = D;
+    p.grp = grp; p.i_gs = i_gs; p.i_go = i_go; p.o_gs = o_gs; p.o_go = o_go;
+    p.w2 = w2; p.b2 = b2; p.rope_cos = rc; p.rope_sin = rs; p.rope_P = rope_P;
+    const double bytes = (double)rows * D * (4.0 + (out_bf16 ? 2.0 : 4.0));
+    return timed(h, s, tag, 0.0, bytes, [&] { return ce::launch_layernorm(p, out_bf16, s); });
+}
+
+int act_code(const ce_handle* h) { return h->cfg.activation == CE_ACT_QUICK_GELU ? ce::ACT_QGELU_ : ce::ACT_GELU_; }
+
+// one pre-LN residual block (transformer.py:257-268) on the f32 stream w.x [B*L][D]
+int run_block(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, int B, int L, int D, int H,
+              int F, bool causal, bool vis) {
+    const int M = B * L;
+    CE_TRY(layernorm(h, s, vis ? "ln_v" : "ln_t", w.x, w.xn, true, k.ln1w, k.ln1b, M, D));
+    CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, k.wqkv, M, 3 * D, D, k.bqkv, ce::ACT_NONE_,
+                nullptr, w.qkv, true));
+    {
+        // algorithmic attention work: QK^T and PV over the full L x L score matrix
+        const double flops = 4.0 * B * H * (double)L * L * 64;
+        const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
+        CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
+                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, causal, s); }));
+    }
+    CE_TRY(gemm(h, s, vis ? "gemm_out_v" : "gemm_out_t", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, w.x,
+                w.x, false));
+    CE_TRY(layernorm(h, s, vis ? "ln_v" : "ln_t", w.x, w.xn, true, k.ln2w, k.ln2b, M, D));
+    CE_TRY(gemm(h, s, vis ? "gemm_fc_v" : "gemm_fc_t", w.xn, D, k.wfc, M, F, D, k.bfc, act_code(h), nullptr,
+                w.hid, true));
+    CE_TRY(gemm(h, s, vis ? "gemm_proj_v" : "gemm_proj_t", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_,
+                w.x, w.x, false));
+    return CE_OK;
+}
+
+int check_launch(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(CE_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return CE_OK;
+}
+
+// Vision tower.  Leaves the final residual stream in w.x.  out_pooled may be null.
+int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, bool pix_bf16, int B,
+               float* out_pooled, bool normalize) {
+    const ce_config& c = h->cfg;
+    const int D = c.vision.width, G = h->G, P = G * G, Lv = P + 1;
+    // _embeds: conv1 as a patch GEMM whose epilogue scatters row (b,p) to b*Lv+1+p and adds pos[1+p]
+    CE_TRY(timed(h, s, "im2col", 0.0, (double)B * 3 * c.image_size * c.image_size * (pix_bf16 ? 2 : 4) +
+                                          (double)B * P * h->Kp * 2,
+                 [&] { return ce::launch_im2col(pix, pix_bf16, w.hid, B, c.image_size, c.patch_size, h->Kp, s); }));
+    CE_TRY(gemm(h, s, "gemm_patch", w.hid, h->Kp, W<bf16_t>(h, "visual.conv1.weight"), B * P, D, h->Kp, nullptr,
+                ce::ACT_NONE_, W(h, "visual.positional_embedding"), w.x, false, P, Lv, 1, 0, 1));
+    CE_TRY(check_launch(ce::launch_cls_rows(w.x, W(h, "visual.class_embedding"), W(h, "visual.positional_embedding"),
+                                            B, Lv, D, s), "cls_rows"));
+    CE_TRY(layernorm(h, s, "ln_v", w.x, w.x, false, W(h, "visual.ln_pre.weight"), W(h, "visual.ln_pre.bias"),
+                     B * Lv, D));
+    for (int i = 0; i < c.vision.layers; ++i) {
+        const Blk k = block_ptrs(h, "visual.transformer.resblocks." + std::to_string(i) + ".");
+        CE_TRY(run_block(h, s, w, k, B, Lv, D, c.vision.heads, c.vision.mlp_width, false, true));
+    }
+    if (out_pooled) {
+        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, nullptr, (long)Lv * D, B, D,
+                                                 W(h, "visual.ln_post.weight"), W(h, "visual.ln_post.bias"), s),
+                            "ln_post(pool)"));
+        ce::FGemmParams fp{};
+        fp.A = w.pooled; fp.lda = D; fp.B = W(h, "visual.proj"); fp.ldb = c.embed_dim;
+        fp.C = out_pooled; fp.ldc = c.embed_dim; fp.M = B; fp.N = c.embed_dim; fp.K = D; fp.batch = 1;
+        fp.alpha = 1.f;
+        CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "visual.proj"));
+        if (normalize) CE_TRY(check_launch(ce::launch_l2norm(out_pooled, out_pooled, B, c.embed_dim, s), "normalize"));
+    }
+    return CE_OK;
+}
+
+int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, int B, float* out_pooled,
+             bool normalize) {
+    const ce_config& c = h->cfg;
+    const int D = c.text.width, L = c.context_length;
+    CE_TRY(check_launch(ce::launch_text_embed(w.x, ids, W(h, "token_embedding.weight"), W(h, "positional_embedding"),
+                                              B, L, D, c.vocab_size, s), "token_embedding"));
+    for (int i = 0; i < c.text.layers; ++i) {
+        const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(i) + ".");
+        CE_TRY(run_block(h, s, w, k, B, L, D, c.text.heads, c.text.mlp_width, true, false));
+    }
+    if (out_pooled) {
+        CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
+        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, w.rows, D, B, D, W(h, "ln_final.weight"),
+                                                 W(h, "ln_final.bias"), s), "ln_final(pool)"));
+        ce::FGemmParams fp{};
+        fp.A = w.pooled; fp.lda = D; fp.B = W(h, "text_projection"); fp.ldb = c.embed_dim;
+        fp.C = out_pooled; fp.ldc = c.embed_dim; fp.M = B; fp.N = c.embed_dim; fp.K = D; fp.batch = 1;
+        fp.alpha = 1.f;
+        CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "text_projection"));
+        if (normalize) CE_TRY(check_launch(ce::launch_l2norm(out_pooled, out_pooled, B, c.embed_dim, s), "normalize"));
+    }
+    return CE_OK;
+}
+
+void host_rope_tables(int P, int D, std::vector<float>& cs, std::vector<float>& sn) {
+    // mirrors apply_rope's f32 arithmetic: inv_freq = 1/(10000^(2i/D)); angle = pos * inv_freq
+    const int half = D / 2;
+    cs.resize((size_t)P * half);
+    sn.resize((size_t)P * half);
+    for (int i = 0; i < half; ++i) {
+        const float expo = (float)(2 * i) / (float)D;
+        const float inv = 1.0f / (float)pow(10000.0, (double)expo);   // see oracle.apply_rope
+        for (int p = 0; p < P; ++p) {
+            const float ang = (float)p * inv;
+            cs[(size_t)p * half + i] = cosf(ang);
+            sn[(size_t)p * half + i] = sinf(ang);
+        }
+    }
+}
+
+int upload(void** dst, const void* src, size_t bytes) {
+    if (hipMalloc(dst, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(CE_ERR_OOM, "cannot allocate %zu bytes", bytes);
+    }
+    HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return CE_OK;
+}
+
+bool valid_tower(const ce_tower_config& t) {
+    return t.width > 0 && t.layers >= 0 && t.heads > 0 && t.width == t.heads * 64 && t.mlp_width > 0 &&
+           t.width % 256 == 0 && t.width <= 1536 && t.mlp_width % 64 == 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+const char* ce_last_error(void) { return g_err.c_str(); }
+
+const char* ce_version(void) { return "clipembed 0.1.0 gfx950"; }
+
+int ce_create(const ce_config* cfg, int device, ce_handle** out) {
+    if (!cfg || !out) return fail(CE_ERR_INVALID, "ce_create: null argument");
+    *out = nullptr;
+    if (!valid_tower(cfg->vision) || !valid_tower(cfg->text))
+        return fail(CE_ERR_INVALID, "ce_create: tower widths must be heads*64, multiple of 256 (got vision %d/%d, text %d/%d)",
+                    cfg->vision.width, cfg->vision.heads, cfg->text.width, cfg->text.heads);
+    if (cfg->patch_size <= 0 || cfg->image_size <= 0 || cfg->image_size % cfg->patch_size)
+        return fail(CE_ERR_INVALID, "ce_create: image_size %d not a multiple of patch_size %d", cfg->image_size,
+                    cfg->patch_size);
+    if (cfg->embed_dim <= 0 || cfg->embed_dim % 64 || cfg->context_length <= 0 || cfg->vocab_size <= 0)
+        return fail(CE_ERR_INVALID, "ce_create: bad embed_dim/context_length/vocab_size");
+    if (cfg->activation != CE_ACT_GELU_ERF && cfg->activation != CE_ACT_QUICK_GELU)
+        return fail(CE_ERR_INVALID, "ce_create: unknown activation %d", cfg->activation);
+    if (cfg->pacl_dim < 0 || cfg->pacl_dim % 128 || cfg->pacl_dim > 1024)
+        return fail(CE_ERR_INVALID, "ce_create: pacl_dim must be 0 or a multiple of 128 <= 1024");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return fail(CE_ERR_HIP, "ce_create: no HIP device available");
+    }
+    if (device < 0 || device >= ndev) return fail(CE_ERR_INVALID, "ce_create: device %d out of range (%d)", device, ndev);
+    DeviceGuard g(device);
+    ce_handle* h = new ce_handle();
+    h->cfg = *cfg;
+    h->device = device;
+    h->G = cfg->image_size / cfg->patch_size;
+    h->Kp = ((3 * cfg->patch_size * cfg->patch_size) + 63) / 64 * 64;
+    build_specs(h);
+    if (hipMalloc(&h->scratch, 256) != hipSuccess) {
+        delete h;
+        return fail(CE_ERR_OOM, "ce_create: scratch allocation failed");
+    }
+    std::vector<float> cs, sn;
+    const int P = h->G * h->G;
+    host_rope_tables(P, cfg->vision.width, cs, sn);
+    int rc = upload((void**)&h->rc_v, cs.data(), cs.size() * 4);
+    if (rc == CE_OK) rc = upload((void**)&h->rs_v, sn.data(), sn.size() * 4);
+    if (rc == CE_OK && cfg->pacl_dim > 0) {
+        host_rope_tables(P, cfg->pacl_dim, cs, sn);
+        rc = upload((void**)&h->rc_p, cs.data(), cs.size() * 4);
+        if (rc == CE_OK) rc = upload((void**)&h->rs_p, sn.data(), sn.size() * 4);
+    }
+    if (rc != CE_OK) {
+        ce_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return CE_OK;
+}
+
+int ce_destroy(ce_handle* h) {
+    if (!h) return CE_OK;
+    DeviceGuard g(h->device);
+    (void)hipDeviceSynchronize();
+    for (auto& kv : h->dptr) (void)hipFree(kv.second);
+    if (h->ws) (void)hipFree(h->ws);
+    if (h->tmp) (void)hipFree(h->tmp);
+    if (h->scratch) (void)hipFree(h->scratch);
+    for (float* p : {h->rc_v, h->rs_v, h->rc_p, h->rs_p})
+        if (p) (void)hipFree(p);
+    for (auto& p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : h->free_ev) (void)hipEventDestroy(e);
+    delete h;
+    return CE_OK;
+}
+
+int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) {
+    if (!h || (n > 0 && !t)) return fail(CE_ERR_INVALID, "ce_load_weights: null argument");
+    DeviceGuard g(h->device);
+    std::vector<float> f;
+    for (int i = 0; i < n; ++i) {
+        if (!t[i].name) return fail(CE_ERR_INVALID, "ce_load_weights: tensor %d has no name", i);
+        const std::string name = canonical(h, t[i].name);
+        auto it = h->specs.find(name);
+        if (it == h->specs.end()) {
+            if (allow_unknown) continue;
+            return fail(CE_ERR_INVALID, "ce_load_weights: unknown weight '%s'", t[i].name);
+        }
+        const WSpec& sp = it->second;
+        // shape check
+        bool ok;
+        if (sp.st == ST_SCALAR) {
+            ok = t[i].ndim == 0 || (t[i].ndim == 1 && t[i].shape[0] == 1);
+        } else {
+            ok = t[i].ndim == (int)sp.shape.size();
+            for (int d = 0; ok && d < t[i].ndim; ++d) ok = t[i].shape[d] == sp.shape[d];
+        }
+        if (!ok) {
+            std::string got, want;
+            for (int d = 0; d < t[i].ndim && d < 4; ++d) got += std::to_string(t[i].shape[d]) + ",";
+            for (auto v : sp.shape) want += std::to_string(v) + ",";
+            return fail(CE_ERR_INVALID, "ce_load_weights: '%s' has shape [%s] expected [%s]", t[i].name,
+                        got.c_str(), want.c_str());
+        }
+        if (!t[i].data) return fail(CE_ERR_INVALID, "ce_load_weights: '%s' has no data", t[i].name);
+        size_t cnt = 1;
+        for (auto v : sp.shape) cnt *= (size_t)v;
+        f.resize(cnt);
+        switch (t[i].dtype) {
+            case CE_F32: memcpy(f.data(), t[i].data, cnt * 4); break;
+            case CE_BF16: {
+                const uint16_t* s = (const uint16_t*)t[i].data;
+                for (size_t j = 0; j < cnt; ++j) f[j] = host_bf2f(s[j]);
+                break;
+            }
+            case CE_F16: {
+                const uint16_t* s = (const uint16_t*)t[i].data;
+                for (size_t j = 0; j < cnt; ++j) f[j] = host_h2f(s[j]);
+                break;
+            }
+            default: return fail(CE_ERR_INVALID, "ce_load_weights: '%s' unsupported dtype %d", t[i].name, t[i].dtype);
+        }
+        std::vector<char> bytes;
+        switch (sp.st) {
+            case ST_SCALAR:
+                h->logit_scale = f[0];
+                h->loaded[name] = true;
+                continue;
+            case ST_F32:
+                bytes.resize(cnt * 4);
+                memcpy(bytes.data(), f.data(), cnt * 4);
+                break;
+            case ST_BF16: {
+                bytes.resize(cnt * 2);
+                uint16_t* o = (uint16_t*)bytes.data();
+                for (size_t j = 0; j < cnt; ++j) o[j] = host_f2bf(f[j]);
+                break;
+            }
+            case ST_BF16_PADK: {
+                const size_t N = (size_t)sp.shape[0], K = cnt / N, Kp = (size_t)h->Kp;
+                bytes.assign(N * Kp * 2, 0);
+                uint16_t* o = (uint16_t*)bytes.data();
+                for (size_t r = 0; r < N; ++r)
+                    for (size_t k = 0; k < K; ++k) o[r * Kp + k] = host_f2bf(f[r * K + k]);
+                break;
+            }
+            case ST_F32_T: {
+                const size_t R = (size_t)sp.shape[0], C = (size_t)sp.shape[1];
+                bytes.resize(cnt * 4);
+                float* o = (float*)bytes.data();
+                for (size_t r = 0; r < R; ++r)
+                    for (size_t c = 0; c < C; ++c) o[c * R + r] = f[r * C + c];
+                break;
+            }
+        }
+        void*& dp = h->dptr[name];
+        if (!dp) {
+            if (hipMalloc(&dp, bytes.size()) != hipSuccess) {
+                dp = nullptr;
+                h->dptr.erase(name);
+                (void)hipGetLastError();
+                return fail(CE_ERR_OOM, "ce_load_weights: cannot allocate '%s'", name.c_str());
+            }
+        }
+        HIP_TRY(hipMemcpy(dp, bytes.data(), bytes.size(), hipMemcpyHostToDevice));
+        h->loaded[name] = true;
+    }
+    return CE_OK;
+}
+
+int ce_missing_weights(ce_handle* h, int* n_missing, const char** first_missing) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_missing_weights: null handle");
+    int n = 0;
+    const char* first = nullptr;
+    for (auto& kv : h->specs)
+        if (kv.second.required && !h->loaded[kv.first]) {
+            if (!first) first = kv.first.c_str();
+            ++n;
+        }
+    if (n_missing) *n_missing = n;
+    if (first_missing) *first_missing = first ? first : "";
+    return CE_OK;
+}
+
+int ce_reserve(ce_handle* h, int max_images, int max_texts) {
+    if (!h || max_images < 0 || max_texts < 0) return fail(CE_ERR_INVALID, "ce_reserve: bad argument");
+    DeviceGuard g(h->device);
+    return ensure_ws(h, std::max(vision_bytes(h, max_images), text_bytes(h, max_texts)));
+}
+
+int ce_encode_image(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int B, int normalize,
+                    float* out_pooled, void* out_tokens, int tokens_dtype) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_encode_image: null handle");
+    if (B <= 0) return fail(CE_ERR_INVALID, "ce_encode_image: batch must be positive (got %d)", B);
+    if (!pixels || (!out_pooled && !out_tokens)) return fail(CE_ERR_INVALID, "ce_encode_image: null buffer");
+    if (pixel_dtype != CE_F32 && pixel_dtype != CE_BF16)
+        return fail(CE_ERR_INVALID, "ce_encode_image: pixels must be f32 or bf16");
+    if (out_tokens && tokens_dtype != CE_F32 && tokens_dtype != CE_BF16)
+        return fail(CE_ERR_INVALID, "ce_encode_image: tokens must be f32 or bf16");
+    CE_TRY(check_ready(h, false));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    CE_TRY(ensure_ws(h, vision_bytes(h, B)));
+    const long P = (long)h->G * h->G, Lv = P + 1;
+    const int D = h->cfg.vision.width;
+    TowerWs w = carve(h->ws, B * Lv, D, h->cfg.vision.mlp_width, B * P * h->Kp, B);
+    CE_TRY(run_vision(h, s, w, pixels, pixel_dtype == CE_BF16, B, out_pooled, normalize != 0));
+    if (out_tokens)
+        CE_TRY(layernorm(h, s, "ln_v", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "visual.ln_post.weight"),
+                         W(h, "visual.ln_post.bias"), (int)(B * P), D, (int)P, (int)Lv, 1, (int)P, 0));
+    return CE_OK;
+}
+
+int ce_encode_text(ce_handle* h, void* stream, const int64_t* ids, int B, int ctx, int normalize,
+                   float* out_pooled, void* out_tokens, int tokens_dtype) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_encode_text: null handle");
+    if (B <= 0) return fail(CE_ERR_INVALID, "ce_encode_text: batch must be positive (got %d)", B);
+    if (ctx != h->cfg.context_length)
+        return fail(CE_ERR_INVALID, "ce_encode_text: context length %d != %d", ctx, h->cfg.context_length);
+    if (!ids || (!out_pooled && !out_tokens)) return fail(CE_ERR_INVALID, "ce_encode_text: null buffer");
+    if (out_tokens && tokens_dtype != CE_F32 && tokens_dtype != CE_BF16)
+        return fail(CE_ERR_INVALID, "ce_encode_text: tokens must be f32 or bf16");
+    CE_TRY(check_ready(h, false));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    CE_TRY(ensure_ws(h, text_bytes(h, B)));
+    const int D = h->cfg.text.width;
+    TowerWs w = carve(h->ws, (long)B * ctx, D, h->cfg.text.mlp_width, 0, B);
+    CE_TRY(run_text(h, s, w, ids, B, out_pooled, normalize != 0));
+    if (out_tokens)
+        CE_TRY(layernorm(h, s, "ln_t", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "ln_final.weight"),
+                         W(h, "ln_final.bias"), B * ctx, D));
+    return CE_OK;
+}
+
+int ce_get_logits(ce_handle* h, void* stream, const float* img, int Bi, const float* txt, int Bt, int D,
+                  float scale, int normalize, float* out_image_logits, float* out_text_logits) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_get_logits: null handle");
+    if (Bi <= 0 || Bt <= 0 || D <= 0) return fail(CE_ERR_INVALID, "ce_get_logits: bad sizes %d %d %d", Bi, Bt, D);
+    if (!img || !txt || !out_image_logits) return fail(CE_ERR_INVALID, "ce_get_logits: null buffer");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const float* a = img;
+    const float* b = txt;
+    if (normalize) {
+        CE_TRY(ensure_tmp(h, ((size_t)Bi + Bt) * D * 4));
+        float* an = (float*)h->tmp;
+        float* bn = an + (size_t)Bi * D;
+        CE_TRY(check_launch(ce::launch_l2norm(an, img, Bi, D, s), "normalize"));
+        CE_TRY(check_launch(ce::launch_l2norm(bn, txt, Bt, D, s), "normalize"));
+        a = an;
+        b = bn;
+    }
+    ce::FGemmParams fp{};
+    fp.A = a; fp.lda = D; fp.B = b; fp.ldb = D; fp.C = out_image_logits; fp.ldc = Bt;
+    fp.M = Bi; fp.N = Bt; fp.K = D; fp.batch = 1; fp.alpha = scale;
+    fp.Ct = out_text_logits; fp.ldct = Bi;
+    return timed(h, s, "logits", 2.0 * Bi * Bt * D, 4.0 * ((double)Bi * D + (double)Bt * D + (double)Bi * Bt),
+                 [&] { return ce::launch_fgemm(fp, true, s); });
+}
+
+int ce_cross_entropy(ce_handle* h, void* stream, const float* logits, int R, int C, const int64_t* labels,
+                     float* out_loss) {
+    if (!h || !logits || !labels || !out_loss) return fail(CE_ERR_INVALID, "ce_cross_entropy: null argument");
+    if (R <= 0 || C <= 0) return fail(CE_ERR_INVALID, "ce_cross_entropy: bad sizes");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(h->scratch, 0, 16, s));
+    CE_TRY(check_launch(ce::launch_cross_entropy_rows(h->scratch, logits, R, C, labels, s), "cross_entropy"));
+    CE_TRY(check_launch(ce::launch_cross_entropy_finish(out_loss, h->scratch, s), "cross_entropy"));
+    return CE_OK;
+}
+
+int ce_pacl_project_patches(ce_handle* h, void* stream, const void* tokens, int tokens_dtype, int B, int P,
+                            int rope, void* out_proj, int out_dtype) {
+    if (!h || !tokens || !out_proj) return fail(CE_ERR_INVALID, "ce_pacl_project_patches: null argument");
+    if (h->cfg.pacl_dim <= 0) return fail(CE_ERR_STATE, "ce_pacl_project_patches: handle has no PACL head");
+    if (tokens_dtype != CE_F32) return fail(CE_ERR_INVALID, "ce_pacl_project_patches: tokens must be f32");
+    if (out_dtype != CE_F32 && out_dtype != CE_BF16) return fail(CE_ERR_INVALID, "ce_pacl_project_patches: out dtype");
+    if (rope != CE_ROPE_NONE && rope != CE_ROPE_BEFORE)
+        return fail(CE_ERR_INVALID, "ce_pacl_project_patches: rope must be NONE or BEFORE");
+    if (B <= 0 || P <= 0) return fail(CE_ERR_INVALID, "ce_pacl_project_patches: bad sizes");
+    if (rope == CE_ROPE_BEFORE && P != h->G * h->G)
+        return fail(CE_ERR_INVALID, "ce_pacl_project_patches: rope tables cover %d patches", h->G * h->G);
+    CE_TRY(check_ready(h, true));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int Dv = h->cfg.vision.width, Pd = h->cfg.pacl_dim;
+    const long M = (long)B * P;
+    // scratch: [rope f32 M*Dv] | xn bf16 M*Dv | lin f32 M*Pd | h1 bf16 M*Pd
+    const size_t need = align256(rope ? M * Dv * 4 : 0) + align256(M * Dv * 2) + align256(M * Pd * 4) + align256(M * Pd * 2);
+    CE_TRY(ensure_ws(h, need));
+    char* p = h->ws;
+    float* rot = (float*)p; p += align256(rope ? M * Dv * 4 : 0);
+    bf16_t* xn = (bf16_t*)p; p += align256(M * Dv * 2);
+    float* lin = (float*)p; p += align256(M * Pd * 4);
+    bf16_t* h1 = (bf16_t*)p;
+    const float* src = (const float*)tokens;
+    if (rope) {
+        CE_TRY(check_launch(ce::launch_rope(rot, src, B, P, Dv, h->rc_v, h->rs_v, s), "apply_rope"));
+        src = rot;
+    }
+    CE_TRY(layernorm(h, s, "ln_pacl", src, xn, true, W(h, "visual_projection.0.weight"), W(h, "visual_projection.0.bias"),
+                     (int)M, Dv));
+    CE_TRY(gemm(h, s, "gemm_pacl", xn, Dv, W<bf16_t>(h, "visual_projection.2.linear_projection.0.weight"), (int)M, Pd,
+                Dv, W(h, "visual_projection.2.linear_projection.0.bias"), ce::ACT_NONE_, nullptr, lin, false));
+    CE_TRY(gemm(h, s, "gemm_pacl", xn, Dv, W<bf16_t>(h, "visual_projection.2.non_linear_projection.0.weight"), (int)M,
+                Pd, Dv, W(h, "visual_projection.2.non_linear_projection.0.bias"), ce::ACT_GELU_, nullptr, h1, true));
+    CE_TRY(gemm(h, s, "gemm_pacl", h1, Pd, W<bf16_t>(h, "visual_projection.2.non_linear_projection.2.weight"), (int)M,
+                Pd, Pd, W(h, "visual_projection.2.non_linear_projection.2.bias"), ce::ACT_NONE_, lin, out_proj,
+                out_dtype == CE_BF16));
+    return CE_OK;
+}
+
+int ce_pacl_project_text(ce_handle* h, void* stream, const float* text_pooled, int B, float* out_proj) {
+    if (!h || !text_pooled || !out_proj) return fail(CE_ERR_INVALID, "ce_pacl_project_text: null argument");
+    if (h->cfg.pacl_dim <= 0) return fail(CE_ERR_STATE, "ce_pacl_project_text: handle has no PACL head");
+    if (B <= 0) return fail(CE_ERR_INVALID, "ce_pacl_project_text: bad batch");
+    CE_TRY(check_ready(h, true));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int E = h->cfg.embed_dim, Pd = h->cfg.pacl_dim;
+    CE_TRY(ensure_tmp(h, (size_t)B * E * 4));
+    float* ln = (float*)h->tmp;
+    CE_TRY(check_launch(ce::launch_ln_gather(ln, text_pooled, nullptr, E, B, E, W(h, "text_projection.0.weight"),
+                                             W(h, "text_projection.0.bias"), s), "pacl text ln"));
+    ce::FGemmParams fp{};
+    fp.A = ln; fp.lda = E; fp.B = W(h, "text_projection.2.weight"); fp.ldb = Pd; fp.C = out_proj; fp.ldc = Pd;
+    fp.M = B; fp.N = Pd; fp.K = E; fp.batch = 1; fp.alpha = 1.f; fp.bias = W(h, "text_projection.2.bias");
+    CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "pacl text linear"));
+    return CE_OK;
+}
+
+int ce_pacl_pool(ce_handle* h, void* stream, const void* visual_proj, int vp_dtype, int Bi, int P,
+                 const float* text_proj, int Bt, int Dp, int weight_mode, int rope_after, float* out_img,
+                 float* out_txt) {
+    if (!h || !visual_proj || !text_proj || !out_img) return fail(CE_ERR_INVALID, "ce_pacl_pool: null argument");
+    if (Bi <= 0 || Bt <= 0 || P <= 0) return fail(CE_ERR_INVALID, "ce_pacl_pool: bad sizes");
+    if (!(Bi == Bt || Bi == 1 || Bt == 1))
+        return fail(CE_ERR_INVALID, "ce_pacl_pool: cannot broadcast %d images against %d texts", Bi, Bt);
+    if (vp_dtype != CE_F32 && vp_dtype != CE_BF16) return fail(CE_ERR_INVALID, "ce_pacl_pool: visual_proj dtype");
+    if (weight_mode != CE_PACL_ONES && weight_mode != CE_PACL_SIGMOID10)
+        return fail(CE_ERR_INVALID, "ce_pacl_pool: unknown weight mode %d", weight_mode);
+    if (rope_after && weight_mode != CE_PACL_SIGMOID10)
+        return fail(CE_ERR_INVALID, "ce_pacl_pool: rope_after only affects the sigmoid10 activations");
+    if (Dp % 128 || Dp > 1024) return fail(CE_ERR_INVALID, "ce_pacl_pool: Dp must be a multiple of 128 <= 1024");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const float *rc = nullptr, *rs = nullptr;
+    std::vector<float> cs, sn;
+    if (rope_after) {
+        if (Dp == h->cfg.pacl_dim && P == h->G * h->G && h->rc_p) { rc = h->rc_p; rs = h->rs_p; }
+        else if (Dp == h->cfg.vision.width && P == h->G * h->G) { rc = h->rc_v; rs = h->rs_v; }
+        else return fail(CE_ERR_INVALID, "ce_pacl_pool: no RoPE table for P=%d D=%d", P, Dp);
+    }
+    const int R = Bi > Bt ? Bi : Bt;
+    return timed(h, s, "pacl_pool", 2.0 * R * P * Dp * (weight_mode ? 2 : 1),
+                 (double)Bi * P * Dp * (vp_dtype == CE_BF16 ? 2 : 4) + 4.0 * Bt * Dp + 4.0 * R * Dp,
+                 [&] { return ce::launch_pacl_pool(visual_proj, vp_dtype == CE_BF16, Bi, P, text_proj, Bt, Dp,
+                                                   weight_mode, rc, rs, out_img, out_txt, s); });
+}
+
+int ce_pacl_forward(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int Bi, const int64_t* ids,
+                    int Bt, int weight_mode, int rope, float* out_img, float* out_txt) {
+    if (!h || !pixels || !ids || !out_img) return fail(CE_ERR_INVALID, "ce_pacl_forward: null argument");
+    if (h->cfg.pacl_dim <= 0) return fail(CE_ERR_STATE, "ce_pacl_forward: handle has no PACL head");
+    if (Bi <= 0 || Bt <= 0) return fail(CE_ERR_INVALID, "ce_pacl_forward: bad sizes");
+    if (!(Bi == Bt || Bi == 1 || Bt == 1))
+        return fail(CE_ERR_INVALID, "ce_pacl_forward: cannot broadcast %d images against %d texts", Bi, Bt);
+    if (pixel_dtype != CE_F32 && pixel_dtype != CE_BF16) return fail(CE_ERR_INVALID, "ce_pacl_forward: pixel dtype");
+    if (rope != CE_ROPE_NONE && rope != CE_ROPE_BEFORE && rope != CE_ROPE_AFTER)
+        return fail(CE_ERR_INVALID, "ce_pacl_forward: unknown rope mode %d", rope);
+    if (rope == CE_ROPE_AFTER && weight_mode != CE_PACL_SIGMOID10)
+        return fail(CE_ERR_INVALID, "ce_pacl_forward: rope AFTER only affects the sigmoid10 activations");
+    CE_TRY(check_ready(h, true));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const ce_config& c = h->cfg;
+    const int E = c.embed_dim, Pd = c.pacl_dim, Dv = c.vision.width;
+    const long P = (long)h->G * h->G, Lv = P + 1;
+    // aux (must survive both towers): tclip [Bt,E] | tp [Bt,Pd]
+    CE_TRY(ensure_ws(h, std::max(vision_bytes(h, Bi), text_bytes(h, Bt))));
+    CE_TRY(ensure_tmp(h, align256((size_t)Bt * E * 4) + align256((size_t)Bt * Pd * 4) + align256((size_t)Bt * E * 4)));
+    float* tclip = (float*)h->tmp;
+    float* tp = (float*)(h->tmp + align256((size_t)Bt * E * 4));
+    // 1) text tower + PACL text head (pacl.py:116-118)
+    {
+        TowerWs w = carve(h->ws, (long)Bt * c.context_length, c.text.width, c.text.mlp_width, 0, Bt);
+        CE_TRY(run_text(h, s, w, ids, Bt, tclip, false));
+        float* ln = (float*)h->tmp + 0;
+        ln = (float*)(h->tmp + align256((size_t)Bt * E * 4) + align256((size_t)Bt * Pd * 4));
+        CE_TRY(check_launch(ce::launch_ln_gather(ln, tclip, nullptr, E, Bt, E, W(h, "text_projection.0.weight"),
+                                                 W(h, "text_projection.0.bias"), s), "pacl text ln"));
+        ce::FGemmParams fp{};
+        fp.A = ln; fp.lda = E; fp.B = W(h, "text_projection.2.weight"); fp.ldb = Pd; fp.C = tp; fp.ldc = Pd;
+        fp.M = Bt; fp.N = Pd; fp.K = E; fp.batch = 1; fp.alpha = 1.f; fp.bias = W(h, "text_projection.2.bias");
+        CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "pacl text linear"));
+    }
+    // 2) vision tower, tokens -> ln_post -> [rope] -> PACL LN (one fused row kernel) -> heads
+    TowerWs w = carve(h->ws, Bi * Lv, Dv, c.vision.mlp_width, Bi * P * h->Kp, Bi);
+    CE_TRY(run_vision(h, s, w, pixels, pixel_dtype == CE_BF16, Bi, nullptr, false));
+    const int M = (int)(Bi * P);
+    CE_TRY(layernorm(h, s, "ln_pacl", w.x, w.xn, true, W(h, "visual.ln_post.weight"), W(h, "visual.ln_post.bias"), M,
+                     Dv, (int)P, (int)Lv, 1, (int)P, 0, W(h, "visual_projection.0.weight"),
+                     W(h, "visual_projection.0.bias"), rope == CE_ROPE_BEFORE ? h->rc_v : nullptr,
+                     rope == CE_ROPE_BEFORE ? h->rs_v : nullptr, (int)P));
+    float* lin = (float*)w.qkv;          // [M, Pd] f32   (fits: Lv*3*Dv*2 >= P*Pd*4)
+    bf16_t* h1 = w.att;                  // [M, Pd] bf16
+    bf16_t* vp = w.hid;                  // [M, Pd] bf16
+    CE_TRY(gemm(h, s, "gemm_pacl", w.xn, Dv, W<bf16_t>(h, "visual_projection.2.linear_projection.0.weight"), M, Pd, Dv,
+                W(h, "visual_projection.2.linear_projection.0.bias"), ce::ACT_NONE_, nullptr, lin, false));
+    CE_TRY(gemm(h, s, "gemm_pacl", w.xn, Dv, W<bf16_t>(h, "visual_projection.2.non_linear_projection.0.weight"), M, Pd,
+                Dv, W(h, "visual_projection.2.non_linear_projection.0.bias"), ce::ACT_GELU_, nullptr, h1, true));
+    CE_TRY(gemm(h, s, "gemm_pacl", h1, Pd, W<bf16_t>(h, "visual_projection.2.non_linear_projection.2.weight"), M, Pd,
+                Pd, W(h, "visual_projection.2.non_linear_projection.2.bias"), ce::ACT_NONE_, lin, vp, true));
+    // 3) fused patch alignment + pooling + normalise
+    return ce_pacl_pool(h, stream, vp, CE_BF16, Bi, (int)P, tp, Bt, Pd, weight_mode, rope == CE_ROPE_AFTER, out_img,
+                        out_txt);
+}
+
+int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l, int B, int P, int T, int D,
+                     float sigma, float* out_grouped, float* out_l_norm, float* out_sim) {
+    if (!h || !v || !l || !out_grouped) return fail(CE_ERR_INVALID, "ce_sparc_forward: null argument");
+    if (B <= 0 || P <= 0 || T <= 0 || D <= 0) return fail(CE_ERR_INVALID, "ce_sparc_forward: bad sizes");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    CE_TRY(ensure_tmp(h, (size_t)B * T * P * 4));
+    float* sim = (float*)h->tmp;
+    ce::FGemmParams a{};
+    a.A = l; a.lda = D; a.sA = (long)T * D;
+    a.B = v; a.ldb = D; a.sB = (long)P * D;
+    a.C = sim; a.ldc = P; a.sC = (long)T * P;
+    a.M = T; a.N = P; a.K = D; a.batch = B; a.alpha = 1.f;
+    CE_TRY(timed(h, s, "sparc_sim", 2.0 * B * T * P * D, 4.0 * B * ((double)T * D + (double)P * D + (double)T * P),
+                 [&] { return ce::launch_fgemm(a, true, s); }));
+    if (out_sim) HIP_TRY(hipMemcpyAsync(out_sim, sim, (size_t)B * T * P * 4, hipMemcpyDeviceToDevice, s));
+    CE_TRY(check_launch(ce::launch_sparc_weights(sim, (long)B * T, P, sigma, s), "sparc weights"));
+    ce::FGemmParams b{};
+    b.A = sim; b.lda = P; b.sA = (long)T * P;
+    b.B = v; b.ldb = D; b.sB = (long)P * D;
+    b.C = out_grouped; b.ldc = D; b.sC = (long)T * D;
+    b.M = T; b.N = D; b.K = P; b.batch = B; b.alpha = 1.f;
+    CE_TRY(timed(h, s, "sparc_group", 2.0 * B * T * P * D, 4.0 * B * ((double)T * P + (double)P * D + (double)T * D),
+                 [&] { return ce::launch_fgemm(b, false, s); }));
+    CE_TRY(check_launch(ce::launch_l2norm(out_grouped, out_grouped, B * T, D, s), "normalize"));
+    if (out_l_norm) CE_TRY(check_launch(ce::launch_l2norm(out_l_norm, l, B * T, D, s), "normalize"));
+    return CE_OK;
+}
+
+int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out) {
+    if (!h || !x || !out) return fail(CE_ERR_INVALID, "ce_apply_rope: null argument");
+    if (B <= 0 || P <= 0 || D <= 0 || D % 2) return fail(CE_ERR_INVALID, "ce_apply_rope: bad sizes");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const float *rc = nullptr, *rs = nullptr;
+    if (P == h->G * h->G && D == h->cfg.vision.width) { rc = h->rc_v; rs = h->rs_v; }
+    else if (P == h->G * h->G && D == h->cfg.pacl_dim) { rc = h->rc_p; rs = h->rs_p; }
+    else return fail(CE_ERR_INVALID, "ce_apply_rope: no RoPE table for P=%d D=%d", P, D);
+    return check_launch(ce::launch_rope(out, x, B, P, D, rc, rs, s), "apply_rope");
+}
+
+int ce_set_kernel_timing(ce_handle* h, int enable) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_set_kernel_timing: null handle");
+    DeviceGuard g(h->device);
+    CE_TRY(resolve_pending(h));
+    h->timing = enable != 0;
+    if (enable) {
+        h->stats.clear();
+        h->stat_idx.clear();
+    }
+    return CE_OK;
+}
+
+int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* total_ms, int64_t* launches,
+                    double* flops, double* bytes) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_kernel_stats: null handle");
+    DeviceGuard g(h->device);
+    CE_TRY(resolve_pending(h));
+    if (index < 0 || index >= (int)h->stats.size()) return fail(CE_ERR_INVALID, "ce_kernel_stats: index out of range");
+    const KStat& k = h->stats[index];
+    if (name && name_len > 0) {
+        strncpy(name, k.name.c_str(), (size_t)name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (total_ms) *total_ms = k.ms;
+    if (launches) *launches = k.n;
+    if (flops) *flops = k.flops;
+    if (bytes) *bytes = k.bytes;
+    return CE_OK;
+}
+
+int ce_kernel_gemm_bf16(void* stream, const void* A, const void* Wt, int M, int N, int K, const float* bias, int act,
+                        const float* resid, void* out, int out_dtype) {
+    if (!A || !Wt || !out) return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16: null argument");
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 64)
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16: need M,N,K > 0, K %% 64 == 0, N %% 64 == 0 (got %d %d %d)", M, N, K);
+    if (act < 0 || act > 2 || (out_dtype != CE_F32 && out_dtype != CE_BF16))
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16: bad act/out dtype");
+    ce::GemmParams p{};
+    p.A = (const bf16_t*)A; p.lda = K; p.W = (const bf16_t*)Wt; p.ldw = K;
+    p.M = M; p.N = N; p.K = K; p.bias = bias; p.resid = resid; p.ldr = N; p.out = out; p.ldo = N;
+    return check_launch(ce::launch_gemm(p, act, out_dtype == CE_BF16, (hipStream_t)stream), "gemm");
+}
+
+int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal) {
+    if (!qkv || !out) return fail(CE_ERR_INVALID, "ce_kernel_attention: null argument");
+    if (B <= 0 || L <= 0 || H <= 0) return fail(CE_ERR_INVALID, "ce_kernel_attention: bad sizes");
+    return check_launch(ce::launch_attention((const bf16_t*)qkv, (bf16_t*)out, B, L, H, causal != 0, (hipStream_t)stream),
+                        "attention");
+}
+
+int ce_kernel_layernorm(void* stream, const float* in, void* out, int out_dtype, const float* w, const float* b,
+                        int rows, int D) {
+    if (!in || !out || !w || !b) return fail(CE_ERR_INVALID, "ce_kernel_layernorm: null argument");
+    if (rows <= 0 || D <= 0 || D % 256 || D > 1536) return fail(CE_ERR_INVALID, "ce_kernel_layernorm: bad sizes");
+    ce::LNParams p{};
+    p.in = in; p.ldi = D; p.out = out; p.ldo = D; p.w = w; p.b = b; p.rows = rows; p.D = D;
+    return check_launch(ce::launch_layernorm(p, out_dtype == CE_BF16, (hipStream_t)stream), "layernorm");
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Device-side helpers shared by the gfx950 kernels of libclipembed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // raw bf16 bits in memory
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;   // MFMA bf16 operand (4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) short s16x4;     // ds_read_b64_tr_b16 result
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define CE_LDS __attribute__((address_space(3)))
+#define CE_GLOBAL __attribute__((address_space(1)))
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+// Round-to-nearest-even, NaN stays NaN (hipcc lowers the cast to v_cvt_pk_bf16_f32).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Exact-erf GELU (torch.nn.GELU default) and QuickGELU (transformer.py:32-35).
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2 };
+
+template <int ACT>
+__device__ __forceinline__ float apply_act(float x) {
+    if constexpr (ACT == ACT_GELU) return gelu_erf(x);
+    else if constexpr (ACT == ACT_QGELU) return quick_gelu(x);
+    else return x;
+}
+
+// Asynchronous 16-byte global -> LDS copy (global_load_lds_dwordx4).  The LDS destination is
+// the wave-uniform `lds_wave_base` + lane*16; the global source is per lane.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const CE_GLOBAL void*)gsrc, (CE_LDS void*)lds_wave_base, 16, 0, 0);
+}

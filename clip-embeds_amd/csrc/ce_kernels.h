@@ -1,0 +1,91 @@
+// Host-side launch interface of the gfx950 kernels (internal to libclipembed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ce {
+
+typedef uint16_t bf16_t;
+
+enum Act { ACT_NONE_ = 0, ACT_GELU_ = 1, ACT_QGELU_ = 2 };
+
+// out[map_o(m)][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) + resid[map_r(m)][n]
+//   A [M][K] bf16 (row stride lda), W [N][K] bf16 (nn.Linear layout, row stride ldw).
+//   map_x(m) = (m / grp) * x_gs + x_go + (m % grp); grp == 0 means the identity map.
+// Requirements (checked by the launcher): K % 64 == 0, N % 64 == 0, 16-B aligned rows.
+struct GemmParams {
+    const bf16_t* A; long lda;
+    const bf16_t* W; long ldw;
+    int M, N, K;
+    const float* bias;                 // nullable, [N]
+    const float* resid; long ldr;      // nullable, f32
+    void* out; long ldo;               // f32 or bf16
+    int grp, o_gs, o_go, r_gs, r_go;
+};
+hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s);
+
+// Multi-head attention over a packed QKV activation.
+//   qkv [B*L][3*D] bf16 (q | k | v, head h at columns h*64 .. h*64+63 of each part)
+//   out [B*L][D]   bf16 (heads concatenated), softmax(q k^T / sqrt(64) [+ causal]) v
+hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal,
+                            hipStream_t s);
+
+// LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.
+//   in row  = (r / grp) * i_gs + i_go + r % grp   (grp == 0: identity)
+//   out row = (r / grp) * o_gs + o_go + r % grp
+struct LNParams {
+    const float* in; long ldi;
+    void* out; long ldo;
+    const float* w; const float* b;
+    int rows, D;
+    int grp, i_gs, i_go, o_gs, o_go;
+    // optional second LayerNorm applied to the first one's output (PACL head LN), with an
+    // optional de-interleaving RoPE between the two (pacl.py:147-181; cos/sin [P][D/2]).
+    const float* w2; const float* b2;
+    const float* rope_cos; const float* rope_sin; int rope_P;
+};
+hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s);
+
+// Patchify: pixels [B,3,S,S] (f32 or bf16) -> cols [B*G*G][Kp] bf16, col = c*p*p + ky*p + kx,
+// zero padded up to Kp.
+hipError_t launch_im2col(const void* pix, bool pix_bf16, bf16_t* cols, int B, int S, int patch,
+                         int Kp, hipStream_t s);
+// x[b*Lv][:] = class_emb + pos[0]  (row 0 of every image)
+hipError_t launch_cls_rows(float* x, const float* cls, const float* pos, int B, int Lv, int D,
+                           hipStream_t s);
+// x[b*ctx+t][:] = tok[ids[b,t]] + pos[t]
+hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, const float* pos,
+                             int B, int ctx, int D, int vocab, hipStream_t s);
+// rows[b] = b*ctx + argmax_t ids[b,t]  (first maximal id; EOT is the largest id)
+hipError_t launch_argmax_rows(int* rows, const int64_t* ids, int B, int ctx, hipStream_t s);
+// LayerNorm of gathered rows: out[i] = LN(x + rows[i]*row_stride) (f32); rows == nullptr -> rows[i] = i
+hipError_t launch_ln_gather(float* out, const float* x, const int* rows, long row_stride, int n,
+                            int D, const float* w, const float* b, hipStream_t s);
+// Batched f32 GEMM (VALU, 64x64 tiles): C[z][i][j] = alpha * sum_k A[z][i][k] * B'[z] + bias[j]
+//   b_nk: B stored [N][K] (C = A B^T) else [K][N] (C = A B).
+struct FGemmParams {
+    const float* A; long lda, sA;
+    const float* B; long ldb, sB;
+    float* C; long ldc, sC;
+    int M, N, K, batch;
+    float alpha;
+    const float* bias;     // nullable [N]
+    float* Ct; long ldct;  // nullable: also write C^T (batch 1 only)
+};
+hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s);
+// rows of D: x / max(||x||, 1e-12)
+hipError_t launch_l2norm(float* out, const float* x, int rows, int D, hipStream_t s);
+// cross entropy: accum[2] (zeroed by the caller) collects sum/count, finish writes the mean
+hipError_t launch_cross_entropy_rows(float* accum, const float* logits, int R, int C,
+                                     const int64_t* labels, hipStream_t s);
+hipError_t launch_cross_entropy_finish(float* loss, const float* accum, hipStream_t s);
+hipError_t launch_pacl_pool(const void* vp, bool vp_bf16, int Bi, int P, const float* tp, int Bt,
+                            int D, int weight_mode, const float* rope_cos, const float* rope_sin,
+                            float* out_img, float* out_txt, hipStream_t s);
+// SPARC row step in place on sim [rows][P]: min-max normalise, zero below sigma, divide by sum
+hipError_t launch_sparc_weights(float* sim, long rows, int P, float sigma, hipStream_t s);
+hipError_t launch_rope(float* out, const float* x, int B, int P, int D, const float* cos_t,
+                       const float* sin_t, hipStream_t s);
+hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t s);
+
+}  // namespace ce

@@ -1,0 +1,200 @@
+// bf16 MFMA GEMM with fused epilogues for gfx950 (CDNA4).
+//
+// Computes every nn.Linear / patch-conv of the CLIP towers (open_clip transformer.py:228,235-239,
+// 549-555 — in_proj, out_proj, c_fc, c_proj, conv1) as  out = act(A W^T + bias) + resid
+// with A = activations [M][K] and W = nn.Linear weight [N][K], both K-contiguous.
+//
+// Design:
+//  * 256x256 output tile per 512-thread workgroup (8 waves, 2 along M x 4 along N, each wave
+//    128(M) x 64(N) = 8x4 MFMA tiles of v_mfma_f32_16x16x32_bf16, 128 f32 accumulators/lane).
+//  * BK = 64; A and W tiles (32 KB each) are staged global->LDS with global_load_lds_dwordx4
+//    into a 2-stage ring (128 KB LDS, one workgroup per CU); the stage for tile t+2 is issued
+//    right after tile t is consumed, so each load has a full tile of MFMA work to land.
+//    Waits are counted (vmcnt(8) = one stage in flight) around raw s_barriers.
+//  * LDS image: 128-B rows, 16-B chunk c of row r stored at chunk c ^ ((r>>1)&7) — makes the
+//    16-lane ds_read_b128 groups bank-conflict free.  The global source address carries the
+//    inverse permutation (glds writes lane-linearly).
+//  * Operands are swapped in the MFMA (W fragment as A, activation fragment as B) so each lane
+//    ends with 4 consecutive output columns of one row: the epilogue does 16-B f32 / 8-B bf16
+//    stores and float4 bias/residual loads.
+//  * Workgroup -> tile map is XCD-aware (bijective round-robin remap): consecutive tiles of one
+//    A row-panel land on the same XCD and share its L2.
+#include "ce_device.h"
+#include "ce_kernels.h"
+
+namespace ce {
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int TILE_BYTES = BM * BK * 2;        // 32 KB per operand tile (BM == BN)
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A + W
+constexpr int LOADS_PER_STAGE = 8;             // glds instructions per thread per stage
+
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+__device__ __forceinline__ void barrier() {
+    compiler_fence();
+    __builtin_amdgcn_s_barrier();
+    compiler_fence();
+}
+
+__device__ __forceinline__ int map_row(int m, int grp, int gs, int go) {
+    if (grp == 0) return m;
+    const int g = m / grp;
+    return g * gs + go + (m - g * grp);
+}
+
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2;   // 0..1 : 128-row slab
+    const int wn = wave & 3;    // 0..3 : 64-col slab
+
+    // ---- XCD-aware bijective tile remap -------------------------------------------------
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tm = wgid / tiles_n;
+    const int tn = wgid - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // ---- staging addresses: thread -> (row tid>>3 of a 64-row pass, 16-B chunk) ---------
+    const int srow = tid >> 3;
+    const int schunk = (tid & 7) ^ ((tid >> 4) & 7);   // inverse of the LDS swizzle
+    const bf16_t* a_src[4];
+    const bf16_t* w_src[4];
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+        int ar = min(m0 + ps * 64 + srow, p.M - 1);
+        int wr = min(n0 + ps * 64 + srow, p.N - 1);
+        a_src[ps] = p.A + (size_t)ar * p.lda + schunk * 8;
+        w_src[ps] = p.W + (size_t)wr * p.ldw + schunk * 8;
+    }
+    const int lds_wave_off = wave * 1024;
+
+    auto stage = [&](int kt, int buf) {
+        char* base = smem + buf * STAGE_BYTES + lds_wave_off;
+        const int koff = kt * BK;
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) glds16(a_src[ps] + koff, base + ps * 8192);
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) glds16(w_src[ps] + koff, base + TILE_BYTES + ps * 8192);
+    };
+
+    // ---- fragment read offsets (per lane, per k-step) ----------------------------------
+    const int fr = lane & 15;
+    const int fq = lane >> 4;
+    const int frag_off0 = fr * 128 + ((((0 * 4) + fq) ^ (fr >> 1)) << 4);
+    const int frag_off1 = fr * 128 + ((((1 * 4) + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 64 * 128;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.K / BK;
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+        const char* sb = smem + (kt & 1) * STAGE_BYTES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int fo = ks ? frag_off1 : frag_off0;
+            bf16x8 af[8], wf[4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                af[i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 128 + fo);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                wf[j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 128 + fo);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+        }
+        // every wave's fragment reads of this buffer must have landed before it is restaged
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+        if (kt + 2 < nk) stage(kt + 2, kt & 1);
+    }
+
+    // ---- epilogue: lane holds C[m = lane&15][n = 4*(lane>>4) .. +3] of each 16x16 tile ---
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + fr;
+        if (m >= p.M) continue;
+        const int orow = map_row(m, p.grp, p.o_gs, p.o_go);
+        int rrow = 0;
+        if constexpr (HAS_RESID) rrow = map_row(m, p.grp, p.r_gs, p.r_go);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + fq * 4;
+            if (n >= p.N) continue;
+            f32x4 v = acc[i][j];
+            if (p.bias) {
+                const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+            }
+            v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
+            v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
+            if constexpr (HAS_RESID) {
+                const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)rrow * p.ldr + n);
+                v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+            }
+            if constexpr (OUT_BF16) {
+                uint2 o;
+                o.x = pack_bf2(v[0], v[1]);
+                o.y = pack_bf2(v[2], v[3]);
+                *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + (size_t)orow * p.ldo + n) = o;
+            } else {
+                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)orow * p.ldo + n) =
+                    make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+hipError_t launch_t(const GemmParams& p, hipStream_t s) {
+    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s) {
+    if (p.M <= 0 || p.N <= 0) return hipSuccess;
+    if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
+    const bool res = p.resid != nullptr;
+#define CE_GEMM_CASE(A_, R_, O_) \
+    if (act == A_ && res == R_ && out_bf16 == O_) return launch_t<A_, R_, O_>(p, s);
+    CE_GEMM_CASE(ACT_NONE, false, true)
+    CE_GEMM_CASE(ACT_NONE, false, false)
+    CE_GEMM_CASE(ACT_NONE, true, true)
+    CE_GEMM_CASE(ACT_NONE, true, false)
+    CE_GEMM_CASE(ACT_GELU, false, true)
+    CE_GEMM_CASE(ACT_QGELU, false, true)
+    CE_GEMM_CASE(ACT_GELU, false, false)
+    CE_GEMM_CASE(ACT_QGELU, false, false)
+#undef CE_GEMM_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace ce

@@ -1,0 +1,352 @@
+// Row-wise HBM-bound kernels of the CLIP towers for gfx950: LayerNorm (optionally LN -> RoPE ->
+// LN for the PACL head), patchify (im2col), class/positional embeddings, token embedding
+// gather, EOT pooling, L2 normalisation, cross-entropy.
+//
+// Reference semantics:
+//   LayerNorm          open_clip/src/open_clip/transformer.py:23-29 (eps 1e-5, biased var)
+//   conv1 patchify     transformer.py:549-555,702-704 (14x14/14, no bias; flatten c,ky,kx)
+//   cls + pos          transformer.py:707-709
+//   token embedding    model.py:286-288
+//   argmax pooling     transformer.py:848-851 (torch.argmax -> first maximal index)
+//   F.normalize        model.py:281,300 (x / max(||x||, 1e-12))
+//   apply_rope         Patch-Aligned-Contrastive-Learning/model/pacl.py:147-181
+//   cross_entropy      loss.py:188-191 (mean over rows, ignore_index -100)
+#include "ce_device.h"
+#include "ce_kernels.h"
+
+namespace ce {
+namespace {
+
+__device__ __forceinline__ int map_row(int r, int grp, int gs, int go) {
+    if (grp == 0) return r;
+    const int g = r / grp;
+    return g * gs + go + (r - g * grp);
+}
+
+template <int NC>
+__device__ __forceinline__ void ln_inplace(float4 (&v)[NC], int D, const float* __restrict__ w,
+                                           const float* __restrict__ b, int lane) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        v[c].x -= mean; v[c].y -= mean; v[c].z -= mean; v[c].w -= mean;
+        q += (v[c].x * v[c].x + v[c].y * v[c].y) + (v[c].z * v[c].z + v[c].w * v[c].w);
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + 1e-5f);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int e = c * 256 + lane * 4;
+        const float4 ww = *reinterpret_cast<const float4*>(w + e);
+        const float4 bb = *reinterpret_cast<const float4*>(b + e);
+        v[c].x = v[c].x * rstd * ww.x + bb.x;
+        v[c].y = v[c].y * rstd * ww.y + bb.y;
+        v[c].z = v[c].z * rstd * ww.z + bb.z;
+        v[c].w = v[c].w * rstd * ww.w + bb.w;
+    }
+}
+
+// One wave per row; 4 rows per 256-thread block.  D = NC * 256.
+template <int NC, bool OUT_BF16, bool DOUBLE, bool ROPE>
+__global__ __launch_bounds__(256) void layernorm_k(LNParams p) {
+    __shared__ float rbuf[ROPE ? 4 * NC * 256 : 1];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= p.rows) return;
+    const int D = NC * 256;
+    const int irow = map_row(row, p.grp, p.i_gs, p.i_go);
+    const int orow = map_row(row, p.grp, p.o_gs, p.o_go);
+    const float* x = p.in + (size_t)irow * p.ldi;
+    float4 v[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v[c] = *reinterpret_cast<const float4*>(x + c * 256 + lane * 4);
+    ln_inplace<NC>(v, D, p.w, p.b, lane);
+    if constexpr (ROPE) {
+        // de-interleave rotate: out[i] = x[2i]c_i - x[2i+1]s_i ; out[D/2+i] = x[2i]s_i + x[2i+1]c_i
+        float* rb = rbuf + wave * NC * 256;
+        const int pos = row % p.rope_P;
+        const float* ct = p.rope_cos + (size_t)pos * (D / 2);
+        const float* st = p.rope_sin + (size_t)pos * (D / 2);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int i0 = c * 128 + lane * 2;
+            const float c0 = ct[i0], s0 = st[i0], c1 = ct[i0 + 1], s1 = st[i0 + 1];
+            rb[i0] = v[c].x * c0 - v[c].y * s0;
+            rb[D / 2 + i0] = v[c].x * s0 + v[c].y * c0;
+            rb[i0 + 1] = v[c].z * c1 - v[c].w * s1;
+            rb[D / 2 + i0 + 1] = v[c].z * s1 + v[c].w * c1;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[c] = *reinterpret_cast<const float4*>(rb + c * 256 + lane * 4);
+    }
+    if constexpr (DOUBLE) ln_inplace<NC>(v, D, p.w2, p.b2, lane);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int e = c * 256 + lane * 4;
+        if constexpr (OUT_BF16) {
+            uint2 o;
+            o.x = pack_bf2(v[c].x, v[c].y);
+            o.y = pack_bf2(v[c].z, v[c].w);
+            *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + (size_t)orow * p.ldo + e) = o;
+        } else {
+            *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)orow * p.ldo + e) = v[c];
+        }
+    }
+}
+
+template <int NC>
+hipError_t ln_dispatch_nc(const LNParams& p, bool out_bf16, hipStream_t s) {
+    const dim3 grid((p.rows + 3) / 4);
+    const bool dbl = p.w2 != nullptr;
+    const bool rope = p.rope_cos != nullptr;
+    if (rope && !dbl) return hipErrorInvalidValue;
+    if (out_bf16) {
+        if (rope) hipLaunchKernelGGL((layernorm_k<NC, true, true, true>), grid, dim3(256), 0, s, p);
+        else if (dbl) hipLaunchKernelGGL((layernorm_k<NC, true, true, false>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((layernorm_k<NC, true, false, false>), grid, dim3(256), 0, s, p);
+    } else {
+        if (rope) hipLaunchKernelGGL((layernorm_k<NC, false, true, true>), grid, dim3(256), 0, s, p);
+        else if (dbl) hipLaunchKernelGGL((layernorm_k<NC, false, true, false>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((layernorm_k<NC, false, false, false>), grid, dim3(256), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+// ---- patchify ---------------------------------------------------------------------------
+template <bool PIX_BF16>
+__global__ __launch_bounds__(256) void im2col_k(const void* __restrict__ pix, bf16_t* __restrict__ cols,
+                                                int B, int S, int patch, int Kp) {
+    const int G = S / patch;
+    const long total = (long)B * G * G * Kp;
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int col = (int)(idx % Kp);
+    const long row = idx / Kp;
+    const int pp2 = patch * patch;
+    float val = 0.f;
+    if (col < 3 * pp2) {
+        const int b = (int)(row / (G * G));
+        const int pidx = (int)(row % (G * G));
+        const int py = pidx / G, px = pidx % G;
+        const int c = col / pp2, rem = col % pp2;
+        const int ky = rem / patch, kx = rem % patch;
+        const size_t off = (((size_t)b * 3 + c) * S + (size_t)(py * patch + ky)) * S + px * patch + kx;
+        if constexpr (PIX_BF16) val = bf2f(static_cast<const bf16_t*>(pix)[off]);
+        else val = static_cast<const float*>(pix)[off];
+    }
+    cols[idx] = f2bf(val);
+}
+
+__global__ __launch_bounds__(256) void cls_rows_k(float* x, const float* cls, const float* pos, int B,
+                                                  int Lv, int D) {
+    const int b = blockIdx.y;
+    const int d = blockIdx.x * 256 + threadIdx.x;
+    if (d < D) x[(size_t)b * Lv * D + d] = cls[d] + pos[d];
+}
+
+__global__ __launch_bounds__(256) void text_embed_k(float* x, const int64_t* ids, const float* tok,
+                                                    const float* pos, int B, int ctx, int D, int vocab) {
+    const int row = blockIdx.x;   // b*ctx + t
+    const int t = row % ctx;
+    int64_t id = ids[row];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    const float* tr = tok + (size_t)id * D;
+    const float* pr = pos + (size_t)t * D;
+    float* xr = x + (size_t)row * D;
+    for (int d = threadIdx.x * 4; d < D; d += 1024) {
+        const float4 a = *reinterpret_cast<const float4*>(tr + d);
+        const float4 c = *reinterpret_cast<const float4*>(pr + d);
+        *reinterpret_cast<float4*>(xr + d) = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w);
+    }
+}
+
+__global__ __launch_bounds__(64) void argmax_rows_k(int* rows, const int64_t* ids, int B, int ctx) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    int64_t best = INT64_MIN;
+    int bidx = ctx;
+    for (int t = lane; t < ctx; t += 64) {
+        const int64_t v = ids[(size_t)b * ctx + t];
+        if (v > best) { best = v; bidx = t; }
+    }
+    // reduce: larger value wins, ties -> smaller index
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bidx, o, 64);
+        if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+    }
+    if (lane == 0) rows[b] = b * ctx + bidx;
+}
+
+// LayerNorm of gathered rows into a compact f32 buffer (pooled tokens), any D % 4 == 0, D <= 4096.
+__global__ __launch_bounds__(256) void ln_gather_k(float* out, const float* x, const int* rows,
+                                                   long row_stride, int n, int D, const float* w,
+                                                   const float* b) {
+    __shared__ float red[2][4];
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const float* src = x + (size_t)(rows ? rows[i] : i) * row_stride;
+    float s = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) s += src[d];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = s;
+    __syncthreads();
+    const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)D;
+    float q = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) { const float t = src[d] - mean; q += t * t; }
+    q = wave_sum(q);
+    if ((threadIdx.x & 63) == 0) red[1][threadIdx.x >> 6] = q;
+    __syncthreads();
+    const float rstd = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)D + 1e-5f);
+    for (int d = threadIdx.x; d < D; d += 256) out[(size_t)i * D + d] = (src[d] - mean) * rstd * w[d] + b[d];
+}
+
+__global__ __launch_bounds__(256) void l2norm_k(float* out, const float* x, int rows, int D) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + (size_t)row * D;
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) s += xr[d] * xr[d];
+    s = wave_sum(s);
+    const float inv = 1.0f / fmaxf(sqrtf(s), 1e-12f);
+    for (int d = lane; d < D; d += 64) out[(size_t)row * D + d] = xr[d] * inv;
+}
+
+// per-row CE: accum[0] += lse - logit[label], accum[1] += 1 (rows with label != -100)
+__global__ __launch_bounds__(256) void ce_rows_k(float* accum, const float* logits, int R, int C,
+                                                 const int64_t* labels) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= R) return;
+    const int64_t lab = labels[row];
+    if (lab == -100) return;
+    const float* lr = logits + (size_t)row * C;
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lr[c]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += expf(lr[c] - mx);
+    s = wave_sum(s);
+    if (lane == 0) {
+        const float loss = (logf(s) + mx) - lr[lab];
+        atomicAdd(&accum[0], loss);
+        atomicAdd(&accum[1], 1.0f);
+    }
+}
+__global__ void ce_finish_k(float* loss, const float* accum) {
+    loss[0] = accum[1] > 0.f ? accum[0] / accum[1] : NAN;
+}
+
+__global__ __launch_bounds__(256) void rope_k(float* out, const float* x, int B, int P, int D,
+                                              const float* ct, const float* st) {
+    const long row = blockIdx.x;         // b*P + p
+    const int p = (int)(row % P);
+    const float* xr = x + row * D;
+    const int half = D / 2;
+    float lo[8], hi[8];
+    int cnt = 0;
+    for (int i = threadIdx.x; i < half && cnt < 8; i += 256, ++cnt) {
+        const float a = xr[2 * i], bb = xr[2 * i + 1];
+        const float c = ct[(size_t)p * half + i], s = st[(size_t)p * half + i];
+        lo[cnt] = a * c - bb * s;
+        hi[cnt] = a * s + bb * c;
+    }
+    __syncthreads();   // x and out may alias
+    cnt = 0;
+    for (int i = threadIdx.x; i < half && cnt < 8; i += 256, ++cnt) {
+        out[row * D + i] = lo[cnt];
+        out[row * D + half + i] = hi[cnt];
+    }
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_k(bf16_t* out, const float* in, long n) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = f2bf(in[i]);
+}
+
+}  // namespace
+
+hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s) {
+    if (p.rows <= 0) return hipSuccess;
+    if (p.D % 256 != 0) return hipErrorInvalidValue;
+    switch (p.D / 256) {
+        case 2: return ln_dispatch_nc<2>(p, out_bf16, s);
+        case 3: return ln_dispatch_nc<3>(p, out_bf16, s);
+        case 4: return ln_dispatch_nc<4>(p, out_bf16, s);
+        case 5: return ln_dispatch_nc<5>(p, out_bf16, s);
+        case 6: return ln_dispatch_nc<6>(p, out_bf16, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_im2col(const void* pix, bool pix_bf16, bf16_t* cols, int B, int S, int patch,
+                         int Kp, hipStream_t s) {
+    const int G = S / patch;
+    const long total = (long)B * G * G * Kp;
+    const dim3 grid((unsigned)((total + 255) / 256));
+    if (pix_bf16) hipLaunchKernelGGL(im2col_k<true>, grid, dim3(256), 0, s, pix, cols, B, S, patch, Kp);
+    else hipLaunchKernelGGL(im2col_k<false>, grid, dim3(256), 0, s, pix, cols, B, S, patch, Kp);
+    return hipGetLastError();
+}
+
+hipError_t launch_cls_rows(float* x, const float* cls, const float* pos, int B, int Lv, int D,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(cls_rows_k, dim3((D + 255) / 256, B), dim3(256), 0, s, x, cls, pos, B, Lv, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, const float* pos, int B,
+                             int ctx, int D, int vocab, hipStream_t s) {
+    if (D % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(text_embed_k, dim3(B * ctx), dim3(256), 0, s, x, ids, tok, pos, B, ctx, D, vocab);
+    return hipGetLastError();
+}
+
+hipError_t launch_argmax_rows(int* rows, const int64_t* ids, int B, int ctx, hipStream_t s) {
+    hipLaunchKernelGGL(argmax_rows_k, dim3(B), dim3(64), 0, s, rows, ids, B, ctx);
+    return hipGetLastError();
+}
+
+hipError_t launch_ln_gather(float* out, const float* x, const int* rows, long row_stride, int n, int D,
+                            const float* w, const float* b, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ln_gather_k, dim3(n), dim3(256), 0, s, out, x, rows, row_stride, n, D, w, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_l2norm(float* out, const float* x, int rows, int D, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(l2norm_k, dim3((rows + 3) / 4), dim3(256), 0, s, out, x, rows, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_cross_entropy_rows(float* accum, const float* logits, int R, int C,
+                                     const int64_t* labels, hipStream_t s) {
+    hipLaunchKernelGGL(ce_rows_k, dim3((R + 3) / 4), dim3(256), 0, s, accum, logits, R, C, labels);
+    return hipGetLastError();
+}
+hipError_t launch_cross_entropy_finish(float* loss, const float* accum, hipStream_t s) {
+    hipLaunchKernelGGL(ce_finish_k, dim3(1), dim3(1), 0, s, loss, accum);
+    return hipGetLastError();
+}
+
+hipError_t launch_rope(float* out, const float* x, int B, int P, int D, const float* cos_t,
+                       const float* sin_t, hipStream_t s) {
+    if (D % 2 || D / 2 > 8 * 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rope_k, dim3(B * P), dim3(256), 0, s, out, x, B, P, D, cos_t, sin_t);
+    return hipGetLastError();
+}
+
+hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t s) {
+    hipLaunchKernelGGL(f32_to_bf16_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, in, n);
+    return hipGetLastError();
+}
+
+}  // namespace ce

@@ -1,0 +1,223 @@
+/*
+ * clipembed.h — C ABI of the MI355X-native CLIP / PACL / SPARC embedding engine.
+ *
+ * This is the drop-in boundary for the hot path of lst627/CLIP-Embeds.  Every entry point
+ * replaces one reference interface; the citation after each declaration is the reference
+ * symbol (path:line, relative to the reference root) whose behaviour it reproduces.
+ *
+ * Conventions
+ *  - Plain C types only; no torch types cross this boundary.
+ *  - Every call returns an int status (CE_OK == 0).  On failure ce_last_error() returns a
+ *    thread-local, NUL-terminated description of the most recent error on this thread.
+ *  - Tensor arguments of the compute calls are DEVICE pointers owned by the caller.  The
+ *    library owns its weights and its workspace (allocated per handle, grown on demand,
+ *    or up front with ce_reserve()).
+ *  - Every compute call is enqueued on `stream` (a hipStream_t, NULL = the null stream) and
+ *    returns without a host synchronisation.
+ *  - One handle per device.  A handle may be used from any host thread, but calls on one
+ *    handle must not overlap in time (they share the handle's workspace); handles on
+ *    different devices are fully independent (this is how nn.DataParallel-style callers
+ *    drive 8 GPUs from 8 host threads).
+ */
+#ifndef CLIPEMBED_H
+#define CLIPEMBED_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ce_status {
+    CE_OK = 0,
+    CE_ERR_INVALID = 1,   /* bad argument / shape mismatch / unknown weight name            */
+    CE_ERR_HIP = 2,       /* a HIP runtime call failed (message carries hipGetErrorString)    */
+    CE_ERR_STATE = 3,     /* weights missing, handle not ready                               */
+    CE_ERR_OOM = 4        /* device allocation failed                                        */
+};
+
+enum ce_dtype { CE_F32 = 0, CE_BF16 = 1, CE_F16 = 2, CE_I64 = 3, CE_I32 = 4 };
+
+/* Activation of the tower MLPs.  open_clip builds ViT-L-14-336 with exact-erf nn.GELU
+ * (open_clip/src/open_clip/model.py:117,193); QuickGELU is the *-quickgelu config flag
+ * (transformer.py:32-35). */
+enum ce_activation { CE_ACT_GELU_ERF = 0, CE_ACT_QUICK_GELU = 1 };
+
+/* PACL patch weighting (Patch-Aligned-Contrastive-Learning/model/pacl.py:120-145).
+ * CE_PACL_ONES reproduces the "Eval only" overwrite at pacl.py:142 (also :193,:272,:288);
+ * CE_PACL_SIGMOID10 is sigmoid(10*cos(text, patch)) as used by pacl.py:206-207,:362-363. */
+enum ce_pacl_weight { CE_PACL_ONES = 0, CE_PACL_SIGMOID10 = 1 };
+
+/* Where apply_rope (pacl.py:147-181) is applied.  BEFORE = on the 1024-d CLIP patch tokens
+ * before the visual projection (open_clip_pacl_rope, pacl.py:184-197); AFTER = on the
+ * projected 768-d tokens, used only for the patch activations (open_clip_pacl_rope_after,
+ * pacl.py:199-209). */
+enum ce_rope { CE_ROPE_NONE = 0, CE_ROPE_BEFORE = 1, CE_ROPE_AFTER = 2 };
+
+typedef struct ce_tower_config {
+    int width;       /* D                                  (vision 1024, text 768)         */
+    int layers;      /* residual blocks                    (vision 24,   text 12)          */
+    int heads;       /* attention heads, head dim = width/heads must be 64                */
+    int mlp_width;   /* MLP hidden                         (vision 4096, text 3072)        */
+} ce_tower_config;
+
+typedef struct ce_config {
+    int embed_dim;          /* output embedding (768)                                      */
+    int activation;         /* enum ce_activation                                          */
+    int image_size;         /* 336                                                         */
+    int patch_size;         /* 14                                                          */
+    ce_tower_config vision;
+    int context_length;     /* 77                                                          */
+    int vocab_size;         /* 49408                                                       */
+    ce_tower_config text;
+    int pacl_dim;           /* PACL head output dim (768); 0 = no PACL head                */
+} ce_config;
+
+/* One host tensor of an open_clip state dict.  `name` is the state-dict key as produced by
+ * CLIP.state_dict() (open_clip/src/open_clip/model.py:222-300); the prefixes "module." and
+ * "clip_model." (PACL checkpoints, eval_pacl.py:380-388) are stripped.  PACL head keys are
+ * "visual_projection.*" / "text_projection.*" as registered by open_clip_pacl
+ * (pacl.py:70-79).  data points to host memory, C-contiguous. */
+typedef struct ce_tensor {
+    const char* name;
+    const void* data;
+    int dtype;              /* enum ce_dtype: CE_F32, CE_BF16 or CE_F16                    */
+    int ndim;
+    int64_t shape[4];
+} ce_tensor;
+
+typedef struct ce_handle ce_handle;
+
+/* Thread-local description of the last error on the calling thread ("" if none). */
+const char* ce_last_error(void);
+
+/* Library version string, e.g. "clipembed 0.1.0 gfx950". */
+const char* ce_version(void);
+
+/* Create an engine on HIP device `device`.
+ * Replaces: CLIP.__init__ / _build_vision_tower / _build_text_tower
+ *   (open_clip/src/open_clip/model.py:105-255) — the tower geometry only; no weights. */
+int ce_create(const ce_config* cfg, int device, ce_handle** out);
+
+/* Release the handle and all device memory it owns. */
+int ce_destroy(ce_handle* h);
+
+/* Copy (and convert to the engine's device layout) a set of state-dict tensors.
+ * May be called several times; later calls overwrite earlier tensors of the same name.
+ * Replaces: CLIP.load_state_dict via open_clip.factory.load_checkpoint
+ *   (open_clip/src/open_clip/factory.py:171-215); PACL checkpoint loading
+ *   (Patch-Aligned-Contrastive-Learning/eval_pacl.py:380-388).
+ * Unknown names are an error (CE_ERR_INVALID) unless `allow_unknown` != 0. */
+int ce_load_weights(ce_handle* h, const ce_tensor* tensors, int n, int allow_unknown);
+
+/* Number of required CLIP tensors not loaded yet (0 = ready); name of the first one. */
+int ce_missing_weights(ce_handle* h, int* n_missing, const char** first_missing);
+
+/* Pre-allocate the workspace for up to `max_images` images and `max_texts` texts per call
+ * (optional; compute calls grow it on demand, which synchronises the device once). */
+int ce_reserve(ce_handle* h, int max_images, int max_texts);
+
+/* Image tower forward.
+ * Replaces: CLIP.encode_image (open_clip/src/open_clip/model.py:279-281) ->
+ *   VisionTransformer.forward (transformer.py:825-836): _embeds :701-716, 24 x
+ *   ResidualAttentionBlock.forward :257-268, _pool :718-741 ('tok' pool), pooled @ proj.
+ * pixels:      device [B,3,image_size,image_size], dtype CE_F32 or CE_BF16, NCHW.
+ * out_pooled:  device f32 [B, embed_dim]; L2-normalised when normalize != 0.
+ * out_tokens:  optional (NULL = not computed) device [B, grid*grid, width] post-ln_post,
+ *              pre-proj patch tokens (transformer.py:738-739,833-834), dtype tokens_dtype
+ *              (CE_F32 or CE_BF16). */
+int ce_encode_image(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int B,
+                    int normalize, float* out_pooled, void* out_tokens, int tokens_dtype);
+
+/* Text tower forward.
+ * Replaces: CLIP.encode_text (open_clip/src/open_clip/model.py:283-301): token_embedding
+ *   gather + positional_embedding, 12 causal blocks (mask transformer.py:960-966), ln_final,
+ *   argmax (EOT) pooling (transformer.py:839-855), @ text_projection.
+ * ids:         device int64 [B, ctx] (ctx must equal context_length).
+ * out_pooled:  device f32 [B, embed_dim].
+ * out_tokens:  optional device [B, ctx, width] post-ln_final, pre-projection tokens
+ *              (model.py:299-300, output_text_tokens=True), dtype tokens_dtype. */
+int ce_encode_text(ce_handle* h, void* stream, const int64_t* ids, int B, int ctx,
+                   int normalize, float* out_pooled, void* out_tokens, int tokens_dtype);
+
+/* Contrastive logits, fused L2-normalise + scale * I @ T^T.
+ * Replaces: CLIP.get_logits (open_clip/src/open_clip/model.py:303-310); the eval scoring
+ *   100 * I @ T^T (eval_clip.py:61-63,321-323); ClipLoss.get_logits local-loss slices
+ *   (open_clip/src/open_clip/loss.py:155-164; pacl.py:498-501).
+ * img [Bi,D], txt [Bt,D] f32 device; out_image_logits [Bi,Bt]; out_text_logits [Bt,Bi]
+ * (optional, = transpose).  normalize != 0 L2-normalises rows first (F.normalize, eps 1e-12). */
+int ce_get_logits(ce_handle* h, void* stream, const float* img, int Bi, const float* txt,
+                  int Bt, int D, float scale, int normalize, float* out_image_logits,
+                  float* out_text_logits);
+
+/* Symmetric / NegCLIP contrastive cross-entropy over precomputed logits rows.
+ * Replaces: F.cross_entropy(logits, labels) with ignore_index -100 as used by
+ *   ClipLoss.forward (open_clip/src/open_clip/loss.py:172-193, labels :113-135) and the
+ *   PACL ClipLoss (pacl.py:503-514).
+ * logits f32 [R,C] device; labels int64 [R] device (-100 = ignored);
+ * out_loss: device f32 scalar = mean over non-ignored rows of (logsumexp - logit[label]). */
+int ce_cross_entropy(ce_handle* h, void* stream, const float* logits, int R, int C,
+                     const int64_t* labels, float* out_loss);
+
+/* PACL visual / text heads (open_clip_pacl.forward_visual / forward_text, pacl.py:112-118;
+ * heads :70-79; Patch_Projection :35-48).  Dropout is identity (eval).
+ * tokens:   device [B, P, width] CLIP patch tokens (dtype tokens_dtype).
+ * rope:     CE_ROPE_NONE or CE_ROPE_BEFORE (apply_rope on the tokens first, pacl.py:187).
+ * out_proj: device [B, P, pacl_dim], dtype out_dtype (CE_F32 or CE_BF16). */
+int ce_pacl_project_patches(ce_handle* h, void* stream, const void* tokens, int tokens_dtype,
+                            int B, int P, int rope, void* out_proj, int out_dtype);
+int ce_pacl_project_text(ce_handle* h, void* stream, const float* text_pooled, int B,
+                         float* out_proj);
+
+/* Fused PACL patch alignment + pooling + normalisation (pacl.py:120-145, 199-209).
+ * visual_proj [Bi,P,Dp] (vp_dtype), text_proj [Bt,Dp] f32.  Broadcast exactly like the
+ * reference: R = max(Bi,Bt) output rows, row r uses image (Bi==1?0:r) and text
+ * (Bt==1?0:r); Bi and Bt must be equal or one of them 1 (pacl.py:129,143).
+ * out_img [R,Dp] = normalize(sum_p w_p v_p), out_txt [Bt,Dp] = normalize(text_proj). */
+int ce_pacl_pool(ce_handle* h, void* stream, const void* visual_proj, int vp_dtype, int Bi,
+                 int P, const float* text_proj, int Bt, int Dp, int weight_mode, int rope_after,
+                 float* out_img, float* out_txt);
+
+/* Whole PACL forward: encode_image(tokens) -> heads -> encode_text -> heads -> pool.
+ * Replaces open_clip_pacl.forward / _rope.forward / _rope_after.forward (pacl.py:135-209).
+ * rope: enum ce_rope.  out_img [max(Bi,Bt), pacl_dim], out_txt [Bt, pacl_dim] (f32). */
+int ce_pacl_forward(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int Bi,
+                    const int64_t* ids, int Bt, int weight_mode, int rope, float* out_img,
+                    float* out_txt);
+
+/* SPARC fine-grained alignment (sparc.forward, pacl.py:453-478).
+ * v [B,P,D] f32 projected patch embeddings, l [B,T,D] f32 projected token embeddings.
+ * out_grouped [B,T,D] = L2norm(rownorm(threshold(minmax(l v^T), sigma)) v);
+ * out_l_norm  [B,T,D] = L2norm(l) (optional, may be NULL);
+ * out_sim     [B,T,P] optional raw similarity l v^T (may be NULL). */
+int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l, int B, int P,
+                     int T, int D, float sigma, float* out_grouped, float* out_l_norm,
+                     float* out_sim);
+
+/* apply_rope (pacl.py:147-181): de-interleaving rotary embedding over positions 0..P-1.
+ * x, out: device f32 [B,P,D] (may alias). */
+int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out);
+
+/* Kernel timing for roofline reporting: when enabled, every launch of the GEMM / attention
+ * / LayerNorm kernels is bracketed by HIP events on its stream and the elapsed times are
+ * accumulated per kernel tag.  ce_kernel_stats reads them (after a stream sync). */
+int ce_set_kernel_timing(ce_handle* h, int enable);
+int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* total_ms,
+                    int64_t* launches, double* flops, double* bytes);
+
+/* ---- kernel-level entry points (parity tests, micro-benchmarks); no handle, device = current ----
+ * GEMM: out = act(A W^T + bias) + resid.  A [M,K] bf16, W [N,K] bf16 (nn.Linear layout), bias f32 [N]
+ * (nullable), resid f32 [M,N] (nullable), out [M,N] f32 or bf16.  K % 64 == 0, N % 64 == 0.
+ * act: 0 none, 1 GELU(erf), 2 QuickGELU.  (ResidualAttentionBlock linears, transformer.py:228-239) */
+int ce_kernel_gemm_bf16(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
+                        int act, const float* resid, void* out, int out_dtype);
+/* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
+int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);
+/* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */
+int ce_kernel_layernorm(void* stream, const float* in, void* out, int out_dtype, const float* w,
+                        const float* b, int rows, int D);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLIPEMBED_H */

@@ -1,0 +1,238 @@
+"""CPU ORACLE — test infrastructure only.
+
+A float32 NumPy restatement of the reference's hot path, used ONLY by tests/, by
+__graft_entry__.smoke() and by bench.py's cpu_baseline leg as the checker / CPU baseline.
+It is never imported by the product package (clip-embeds_amd/clipembed), never linked into
+libclipembed.so, and is not a fallback.
+
+Parity is PINNED: tests/test_oracle_golden.py checks this module against golden vectors that
+tests/golden/make_golden.py produced by running the reference itself (open_clip CLIP and the
+PACL/SPARC modules of Patch-Aligned-Contrastive-Learning/model/pacl.py, imported from
+/root/reference in the build container) on the same deterministic weights and inputs.
+
+Each function cites the reference code it restates (paths relative to the reference root).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+from scipy.special import erf
+
+F32 = np.float32
+
+
+def layer_norm(x, w, b, eps=1e-5):
+    """LayerNorm / F.layer_norm (open_clip/src/open_clip/transformer.py:23-29): biased variance."""
+    x = x.astype(F32, copy=False)
+    mu = x.mean(-1, keepdims=True, dtype=F32)
+    xc = x - mu
+    var = (xc * xc).mean(-1, keepdims=True, dtype=F32)
+    return (xc / np.sqrt(var + F32(eps)) * w + b).astype(F32)
+
+
+def gelu(x):
+    """nn.GELU() exact erf form (the default act of open_clip towers, model.py:117,193)."""
+    return (F32(0.5) * x * (F32(1.0) + erf(x / F32(math.sqrt(2.0))).astype(F32))).astype(F32)
+
+
+def quick_gelu(x):
+    """QuickGELU (transformer.py:32-35)."""
+    return (x / (F32(1.0) + np.exp(F32(-1.702) * x))).astype(F32)
+
+
+def softmax(x, axis=-1):
+    m = x.max(axis, keepdims=True)
+    e = np.exp(x - m)
+    return (e / e.sum(axis, keepdims=True)).astype(F32)
+
+
+def l2normalize(x, eps=1e-12):
+    """F.normalize(x, dim=-1) (model.py:281,300)."""
+    n = np.sqrt((x.astype(F32) ** 2).sum(-1, keepdims=True))
+    return (x / np.maximum(n, F32(eps))).astype(F32)
+
+
+def mha(x, in_w, in_b, out_w, out_b, heads, causal):
+    """nn.MultiheadAttention(batch_first) self-attention as called by
+    ResidualAttentionBlock.attention (transformer.py:242-255); additive causal -inf mask
+    triu(1) of TextTransformer.build_causal_mask (transformer.py:960-966)."""
+    B, L, D = x.shape
+    hd = D // heads
+    qkv = x @ in_w.T + in_b                                   # [B, L, 3D]
+    q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+    q = q.reshape(B, L, heads, hd).transpose(0, 2, 1, 3)
+    k = k.reshape(B, L, heads, hd).transpose(0, 2, 1, 3)
+    v = v.reshape(B, L, heads, hd).transpose(0, 2, 1, 3)
+    s = (q @ k.transpose(0, 1, 3, 2)) * F32(1.0 / math.sqrt(hd))
+    if causal:
+        s = s + np.triu(np.full((L, L), -np.inf, dtype=F32), 1)
+    p = softmax(s, -1)
+    o = (p @ v).transpose(0, 2, 1, 3).reshape(B, L, D)
+    return (o @ out_w.T + out_b).astype(F32)
+
+
+def block(x, sd, prefix, heads, causal, act):
+    """ResidualAttentionBlock.forward (transformer.py:257-268), ls_1/ls_2 = Identity."""
+    g = lambda n: sd[prefix + n]
+    h = layer_norm(x, g("ln_1.weight"), g("ln_1.bias"))
+    x = x + mha(h, g("attn.in_proj_weight"), g("attn.in_proj_bias"), g("attn.out_proj.weight"),
+                g("attn.out_proj.bias"), heads, causal)
+    h = layer_norm(x, g("ln_2.weight"), g("ln_2.bias"))
+    h = act(h @ g("mlp.c_fc.weight").T + g("mlp.c_fc.bias"))
+    x = x + (h @ g("mlp.c_proj.weight").T + g("mlp.c_proj.bias"))
+    return x.astype(F32)
+
+
+def encode_image(sd: Dict[str, np.ndarray], pixels: np.ndarray, cfg, normalize=False, output_tokens=False):
+    """CLIP.encode_image -> VisionTransformer.forward (model.py:279-281; transformer.py:701-716,
+    718-741, 825-836): conv1 14/14 -> [cls; patches] + pos -> ln_pre -> blocks -> ln_post ->
+    pooled = row 0 ('tok') @ proj; tokens = rows 1.. (post-LN, pre-proj)."""
+    v = cfg.vision
+    B = pixels.shape[0]
+    p, G = v.patch_size, v.grid
+    x = pixels.astype(F32).reshape(B, 3, G, p, G, p).transpose(0, 2, 4, 1, 3, 5).reshape(B, G * G, 3 * p * p)
+    w = sd["visual.conv1.weight"].reshape(v.width, -1)
+    x = x @ w.T                                                      # [B, P, D]
+    cls = np.broadcast_to(sd["visual.class_embedding"], (B, 1, v.width))
+    x = np.concatenate([cls, x], axis=1) + sd["visual.positional_embedding"]
+    x = layer_norm(x, sd["visual.ln_pre.weight"], sd["visual.ln_pre.bias"])
+    act = quick_gelu if cfg.quick_gelu else gelu
+    for i in range(v.layers):
+        x = block(x, sd, f"visual.transformer.resblocks.{i}.", v.heads, False, act)
+    x = layer_norm(x, sd["visual.ln_post.weight"], sd["visual.ln_post.bias"])
+    pooled, tokens = x[:, 0], x[:, 1:]
+    pooled = (pooled @ sd["visual.proj"]).astype(F32)
+    if normalize:
+        pooled = l2normalize(pooled)
+    return (pooled, tokens) if output_tokens else pooled
+
+
+def encode_text(sd: Dict[str, np.ndarray], ids: np.ndarray, cfg, normalize=False, output_tokens=False):
+    """CLIP.encode_text (model.py:283-301): token_embedding + pos, causal blocks, ln_final,
+    argmax (EOT) pooling (transformer.py:848-851), @ text_projection."""
+    t = cfg.text
+    x = sd["token_embedding.weight"][ids] + sd["positional_embedding"]
+    act = quick_gelu if cfg.quick_gelu else gelu
+    for i in range(t.layers):
+        x = block(x, sd, f"transformer.resblocks.{i}.", t.heads, True, act)
+    x = layer_norm(x, sd["ln_final.weight"], sd["ln_final.bias"])
+    pooled = x[np.arange(x.shape[0]), ids.argmax(-1)]
+    pooled = (pooled @ sd["text_projection"]).astype(F32)
+    if normalize:
+        pooled = l2normalize(pooled)
+    return (pooled, x) if output_tokens else pooled
+
+
+def get_logits(img_feat, txt_feat, scale):
+    """CLIP.get_logits on already-normalised features (model.py:303-310)."""
+    il = (F32(scale) * img_feat @ txt_feat.T).astype(F32)
+    return il, il.T.copy()
+
+
+# ------------------------------------------------------------------ PACL (pacl.py)
+def apply_rope(x):
+    """apply_rope (Patch-Aligned-Contrastive-Learning/model/pacl.py:147-181): f32 angles,
+    de-interleaved output [x_even*cos - x_odd*sin, x_even*sin + x_odd*cos]."""
+    B, L, D = x.shape
+    # torch evaluates 10000 ** e with its own f32 pow; a double pow rounded to f32 matches it on
+    # all but a few entries (1 ulp), which positions up to 575 turn into ~3e-5 in sin/cos.
+    e = (np.arange(0, D, 2, dtype=F32) / F32(D)).astype(F32)
+    inv = (F32(1.0) / (10000.0 ** e.astype(np.float64)).astype(F32)).astype(F32)
+    ang = (np.arange(L, dtype=F32)[:, None] * inv[None, :]).astype(F32)
+    s, c = np.sin(ang).astype(F32), np.cos(ang).astype(F32)
+    x1, x2 = x[..., 0::2], x[..., 1::2]
+    return np.concatenate([x1 * c - x2 * s, x1 * s + x2 * c], axis=-1).astype(F32)
+
+
+def pacl_visual_head(h, tokens):
+    """visual_projection = Sequential(LayerNorm, Dropout(eval: id), Patch_Projection) (pacl.py:70-74,
+    35-48): lin(x) + Linear(GELU(Linear(x)))."""
+    x = layer_norm(tokens, h["visual_projection.0.weight"], h["visual_projection.0.bias"])
+    lin = x @ h["visual_projection.2.linear_projection.0.weight"].T + h["visual_projection.2.linear_projection.0.bias"]
+    nl = gelu(x @ h["visual_projection.2.non_linear_projection.0.weight"].T
+              + h["visual_projection.2.non_linear_projection.0.bias"])
+    nl = nl @ h["visual_projection.2.non_linear_projection.2.weight"].T + h["visual_projection.2.non_linear_projection.2.bias"]
+    return (lin + nl).astype(F32)
+
+
+def pacl_text_head(h, text):
+    """text_projection = Sequential(LayerNorm(768), Dropout, Linear(768,768)) (pacl.py:75-79)."""
+    x = layer_norm(text, h["text_projection.0.weight"], h["text_projection.0.bias"])
+    return (x @ h["text_projection.2.weight"].T + h["text_projection.2.bias"]).astype(F32)
+
+
+def pacl_pool(visual_proj, text_proj, weights="ones", rope_after=False):
+    """open_clip_pacl.patch_alignment + forward pooling (pacl.py:120-145, 199-209) with the
+    reference's broadcasting: [Bi,P,D] x [Bt,D] -> R = max(Bi,Bt) rows (Q6)."""
+    Bi, P, D = visual_proj.shape
+    Bt = text_proj.shape[0]
+    R = max(Bi, Bt)
+    tn = l2normalize(text_proj)
+    out = np.zeros((R, D), dtype=F32)
+    act_src = apply_rope(visual_proj) if rope_after else visual_proj
+    for r in range(R):
+        vi = visual_proj[0 if Bi == 1 else r]
+        if weights == "ones":
+            w = np.ones(P, dtype=F32)
+        else:
+            a = l2normalize(act_src[0 if Bi == 1 else r]) @ tn[0 if Bt == 1 else r]
+            w = (F32(1.0) / (F32(1.0) + np.exp(F32(-10.0) * a))).astype(F32)
+        out[r] = (vi * w[:, None]).sum(0)
+    return l2normalize(out), tn
+
+
+def pacl_forward(sd, heads, pixels, ids, cfg, weights="ones", rope="none"):
+    """open_clip_pacl{,_rope,_rope_after}.forward (pacl.py:135-145,184-209)."""
+    _, tokens = encode_image(sd, pixels, cfg, output_tokens=True)
+    if rope == "before":
+        tokens = apply_rope(tokens)
+    vp = pacl_visual_head(heads, tokens)
+    tp = pacl_text_head(heads, encode_text(sd, ids, cfg))
+    return pacl_pool(vp, tp, weights=weights, rope_after=(rope == "after"))
+
+
+# ------------------------------------------------------------------ SPARC (pacl.py:453-478)
+def sparc_forward(v, l, sigma):
+    """similarity einsum -> min-max (1e-8) -> threshold sigma -> row-normalise (1e-8) -> group
+    einsum -> L2 normalise (pacl.py:460-476). v [B,P,D], l [B,T,D]."""
+    sim = np.einsum("btd,bpd->btp", l, v).astype(F32)
+    mn = sim.min(-1, keepdims=True)
+    mx = sim.max(-1, keepdims=True)
+    s = (sim - mn) / (mx - mn + F32(1e-8))
+    s = np.where(s < F32(sigma), F32(0.0), s).astype(F32)
+    w = s / (s.sum(-1, keepdims=True) + F32(1e-8))
+    g = np.einsum("btp,bpd->btd", w, v).astype(F32)
+    return l2normalize(g), l2normalize(l), sim
+
+
+# ------------------------------------------------------------------ losses
+def cross_entropy(logits, labels):
+    """F.cross_entropy mean with ignore_index -100."""
+    m = logits.max(-1, keepdims=True)
+    lse = (np.log(np.exp(logits - m).sum(-1)) + m[:, 0]).astype(np.float64)
+    keep = labels != -100
+    picked = logits[np.arange(len(labels))[keep], labels[keep]]
+    return float((lse[keep] - picked).mean())
+
+
+def pacl_clip_loss(img, txt, temperature=0.1):
+    """PACL ClipLoss (pacl.py:489-514): logit_scale = 1/T."""
+    s = 1.0 / temperature
+    lpi = s * img @ txt.T
+    lpt = s * txt @ img.T
+    lab = np.arange(img.shape[0])
+    return (cross_entropy(lpi, lab) + cross_entropy(lpt, lab)) / 2
+
+
+def negclip_local_loss(imgs, txts, per_rank_B, rank, scale):
+    """open_clip ClipLoss(local_loss=True, usehardtext=True) on rank `rank` (loss.py:137-193):
+    imgs[r] [B,D], txts[r] [B+K_r, D] for every rank r."""
+    all_img = np.concatenate(imgs, 0)
+    all_txt = np.concatenate([t[:per_rank_B] for t in txts] + [t[per_rank_B:] for t in txts], 0)
+    lpi = scale * imgs[rank] @ all_txt.T
+    lpt = scale * txts[rank] @ all_img.T
+    li = np.arange(per_rank_B) + per_rank_B * rank
+    lt = np.concatenate([li, -100 * np.ones(txts[rank].shape[0] - per_rank_B, dtype=np.int64)])
+    return (cross_entropy(lpi, li) + cross_entropy(lpt, lt)) / 2

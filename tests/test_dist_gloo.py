@@ -1,0 +1,67 @@
+"""The multi-GPU exchange step (NegCLIP variable-size all-gather, reorder, local-loss labels:
+open_clip loss.py:67-87,127-164) on 2 CPU ranks over gloo, checked against the reference's
+2-rank losses (tests/golden/negclip.npz).  Logits/CE are evaluated with the oracle here because
+there is no device; on a GPU box the same ClipLoss runs them in libclipembed."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "clip-embeds_amd"), repo]
+    from clipembed import weights as W
+    from clipembed.loss import ClipLoss
+    from oracle import clip_oracle as O
+
+    class CpuCheckedLoss(ClipLoss):     # test double: oracle arithmetic, product exchange logic
+        def _logits(self, a, b, scale):
+            return torch.from_numpy(np.float32(scale) * a.numpy() @ b.numpy().T)
+
+        def _ce(self, logits, labels):
+            return torch.tensor(O.cross_entropy(logits.numpy(), labels.numpy()))
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, D, K = 4, 768, [2, 3][rank]
+    img = torch.from_numpy(O.l2normalize(W.uniform(f"neg-img-{rank}", B * D).reshape(B, D)))
+    txt = torch.from_numpy(O.l2normalize(W.uniform(f"neg-txt-{rank}", (B + K) * D).reshape(B + K, D)))
+    res = {
+        "hard": float(CpuCheckedLoss(local_loss=True, rank=rank, world_size=world, usehardtext=True)(img, txt, 14.2857)),
+        "plain_local": float(CpuCheckedLoss(local_loss=True, rank=rank, world_size=world)(img, txt[:B], 14.2857)),
+        "plain_global": float(CpuCheckedLoss(local_loss=False, rank=rank, world_size=world)(img, txt[:B], 14.2857)),
+    }
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_negclip_exchange_two_ranks(golden):
+    g = golden("negclip")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        for k in ("hard", "plain_local", "plain_global"):
+            np.testing.assert_allclose(got[r][k], float(g[f"{k}_r{r}"]), rtol=1e-5, err_msg=f"{k} rank {r}")

@@ -1,0 +1,121 @@
+"""Kernel-level numerics of the HIP kernels against plain PyTorch fp32 references of the same op,
+called through the C ABI's kernel entry points (include/clipembed.h, ce_kernel_*)."""
+import ctypes
+
+import pytest
+import torch
+
+from clipembed import _lib
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def gemm_ref(A, W, bias, act, resid):
+    y = A.float() @ W.float().t()
+    if bias is not None:
+        y = y + bias
+    if act == 1:
+        y = torch.nn.functional.gelu(y)
+    elif act == 2:
+        y = y * torch.sigmoid(1.702 * y)
+    if resid is not None:
+        y = y + resid
+    return y
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 1024), (4617, 3072, 1024), (1154, 1024, 4096),
+                                   (231, 2304, 768), (5, 768, 1024), (700, 832, 640), (1, 64, 64)])
+@pytest.mark.parametrize("variant", ["bias_bf16", "gelu_bf16", "qgelu_bf16", "resid_f32", "plain_f32"])
+def test_gemm(M, N, K, variant):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV) if variant != "plain_f32" else None
+    resid = torch.randn(M, N, generator=g).to(DEV) if variant == "resid_f32" else None
+    act = {"gelu_bf16": 1, "qgelu_bf16": 2}.get(variant, 0)
+    out_bf16 = variant.endswith("bf16")
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), act, P(resid), P(out),
+              _lib.CE_BF16 if out_bf16 else _lib.CE_F32)
+    torch.cuda.synchronize()
+    ref = gemm_ref(A, W, bias, act, resid)
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    tol = (8e-3 if out_bf16 else 2e-4) * scale + 1e-5   # bf16 output rounding / f32 accumulation order
+    assert err <= tol, f"max err {err} vs tol {tol}"
+
+
+def test_gemm_identity_asymmetric():
+    """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
+    n = 256
+    A = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    W = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
+    out = torch.empty(n, n, device=DEV, dtype=torch.float32)
+    _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), n, n, n, None, 0, None, P(out), _lib.CE_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(out, W.float().t())
+
+
+def attn_ref(qkv, B, L, H, causal):
+    D = H * 64
+    x = qkv.float().reshape(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    s = (q @ k.transpose(-1, -2)) / 8.0
+    if causal:
+        s = s + torch.triu(torch.full((L, L), float("-inf"), device=qkv.device), 1)
+    p = s.softmax(-1)
+    return (p @ v).permute(0, 2, 1, 3).reshape(B * L, D)
+
+
+@pytest.mark.parametrize("B,L,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1, 16, False),
+                                          (2, 64, 4, False), (2, 65, 4, True), (1, 129, 2, False),
+                                          (1, 300, 12, True), (5, 577, 1, False)])
+def test_attention(B, L, H, causal):
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16).to(DEV)
+    out = torch.empty(B * L, H * 64, device=DEV, dtype=torch.bfloat16)
+    _lib.call("ce_kernel_attention", S(), P(qkv), P(out), B, L, H, 1 if causal else 0)
+    torch.cuda.synchronize()
+    ref = attn_ref(qkv, B, L, H, causal)
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_attention_spike_rescale():
+    """Force the online-softmax rescale: a late key dominates one query (guide §5.4 rule 26)."""
+    B, L, H = 1, 577, 2
+    g = torch.Generator(device="cpu").manual_seed(3)
+    qkv = torch.randn(B * L, 3 * H * 64, generator=g) * 0.5
+    D = H * 64
+    qkv[10, 0:64] = 4.0                 # query 10, head 0
+    qkv[500, D:D + 64] = 4.0            # key 500 -> huge score for query 10 at the 8th key tile
+    qkv = qkv.to(torch.bfloat16).to(DEV)
+    out = torch.empty(B * L, D, device=DEV, dtype=torch.bfloat16)
+    _lib.call("ce_kernel_attention", S(), P(qkv), P(out), B, L, H, 0)
+    torch.cuda.synchronize()
+    ref = attn_ref(qkv, B, L, H, False)
+    assert (out.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("rows,D,bf16", [(1000, 1024, True), (1000, 1024, False), (77, 768, True), (3, 768, False)])
+def test_layernorm(rows, D, bf16):
+    g = torch.Generator(device="cpu").manual_seed(rows + D)
+    x = (torch.randn(rows, D, generator=g) * 3 + 1).to(DEV)
+    w = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    out = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16 if bf16 else torch.float32)
+    _lib.call("ce_kernel_layernorm", S(), P(x), P(out), _lib.CE_BF16 if bf16 else _lib.CE_F32, P(w), P(b), rows, D)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.layer_norm(x, (D,), w, b, 1e-5)
+    err = (out.float() - ref).abs().max().item()
+    assert err < (3e-2 if bf16 else 1e-4), err

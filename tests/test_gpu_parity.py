@@ -1,0 +1,251 @@
+"""End-to-end parity of the HIP engine (through the C ABI) against the reference's golden vectors
+(tests/golden, produced by running open_clip / pacl.py) and the pinned CPU oracle.
+
+Tolerance (north_star): the engine computes in bf16 (MFMA, f32 accumulate, f32 residual stream,
+f32 LayerNorm statistics); pooled embeddings must be within 1e-3 cosine distance of the f32
+reference and produce identical top-1 retrieval indices."""
+import numpy as np
+import pytest
+import torch
+
+import clipembed
+from clipembed import ClipEmbedError, weights as W
+from clipembed.config import get_model_config
+from clipembed.pacl import (apply_rope, open_clip_pacl, open_clip_pacl_rope, open_clip_pacl_rope_after,
+                            open_clip_pacl_sigmoid)
+from oracle import clip_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROWS_V = [0, 1, 23, 24, 287, 300, 551, 575]
+ROWS_T = [0, 1, 5, 20, 40, 76]
+COS_TOL = 1e-3
+
+
+def cos_dist(a, b):
+    a = np.asarray(a, np.float64).reshape(-1, a.shape[-1])
+    b = np.asarray(b, np.float64).reshape(-1, b.shape[-1])
+    c = (a * b).sum(-1) / (np.linalg.norm(a, axis=-1) * np.linalg.norm(b, axis=-1))
+    return float((1 - c).max())
+
+
+def make_model(cfg):
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(W.synthetic_state_dict(cfg))
+    return m.to("cuda")
+
+
+@pytest.fixture(scope="module")
+def small():
+    return make_model(get_model_config("ViT-L-14-336").with_depth(2, 2))
+
+
+def test_reduced_depth_vs_golden(small, golden):
+    g = golden("clip_v2t2")
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
+    caps = torch.from_numpy(g["captions"])
+    small.visual.output_tokens = True
+    small.output_text_tokens = True
+    try:
+        pi, ti = small.encode_image(imgs)
+        pt, tt = small.encode_text(caps)
+    finally:
+        small.visual.output_tokens = False
+        small.output_text_tokens = False
+    pi, ti, pt, tt = (x.cpu().numpy() for x in (pi, ti, pt, tt))
+    assert cos_dist(pi, g["image_pooled"]) < COS_TOL
+    assert cos_dist(pt, g["text_pooled"]) < COS_TOL
+    assert cos_dist(ti[:, ROWS_V], g["image_tokens_rows"]) < COS_TOL
+    assert cos_dist(tt[:, ROWS_T], g["text_tokens_rows"]) < COS_TOL
+    il, tl = small.get_logits(imgs, caps)
+    np.testing.assert_allclose(il.cpu().numpy(), g["image_logits"], atol=0.05 * np.abs(g["image_logits"]).max())
+    assert np.array_equal(tl.cpu().numpy(), il.cpu().numpy().T)
+    fi, ft, ls = small(imgs, caps)
+    assert cos_dist(fi.cpu().numpy(), g["image_features"]) < COS_TOL
+    np.testing.assert_allclose(np.linalg.norm(fi.cpu().numpy(), axis=-1), 1.0, rtol=1e-5)
+    np.testing.assert_allclose(float(ls), float(g["logit_scale_exp"]), rtol=1e-6)
+
+
+def test_reduced_depth_vs_oracle_batch(small):
+    """Batch of 5 images / 7 texts (ragged tiles) against the oracle on the same inputs."""
+    cfg = small.cfg
+    sd = W.synthetic_state_dict(cfg)
+    imgs = W.synthetic_images(5, seed=1234)
+    caps = W.synthetic_captions(7, seed=4321)
+    pi = small.encode_image(torch.from_numpy(imgs)).cpu().numpy()
+    pt = small.encode_text(torch.from_numpy(caps)).cpu().numpy()
+    assert cos_dist(pi, O.encode_image(sd, imgs, cfg)) < COS_TOL
+    assert cos_dist(pt, O.encode_text(sd, caps, cfg)) < COS_TOL
+
+
+def test_bf16_pixels(small):
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
+    a = small.encode_image(imgs)
+    b = small.encode_image(imgs.to(torch.bfloat16))
+    assert cos_dist(a.cpu().numpy(), b.cpu().numpy()) < 1e-3
+
+
+def test_quickgelu_vs_golden(golden):
+    cfg = get_model_config("ViT-L-14-336-quickgelu").with_depth(1, 1)
+    m = make_model(cfg)
+    g = golden("clip_quickgelu_v1t1")
+    pi = m.encode_image(torch.from_numpy(W.synthetic_images(2, seed=1000))).cpu().numpy()
+    pt = m.encode_text(torch.from_numpy(g["captions"])).cpu().numpy()
+    assert cos_dist(pi, g["image_pooled"]) < COS_TOL
+    assert cos_dist(pt, g["text_pooled"]) < COS_TOL
+
+
+def test_full_depth_vs_golden(golden):
+    """ViT-L/14-336 at full depth (24 + 12 blocks) vs the reference f32 CPU forward."""
+    cfg = get_model_config("ViT-L-14-336")
+    m = make_model(cfg)
+    g = golden("clip_full")
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
+    caps = torch.from_numpy(g["captions"])
+    m.visual.output_tokens = True
+    pi, ti = m.encode_image(imgs)
+    m.visual.output_tokens = False
+    pt = m.encode_text(caps)
+    assert cos_dist(pi.cpu().numpy(), g["image_pooled"]) < COS_TOL
+    assert cos_dist(pt.cpu().numpy(), g["text_pooled"]) < COS_TOL
+    assert cos_dist(ti.cpu().numpy()[:, ROWS_V], g["image_tokens_rows"]) < COS_TOL
+    il, _ = m.get_logits(imgs, caps)
+    assert (il.cpu().numpy().argmax(1) == g["image_logits"].argmax(1)).all()
+    assert (il.cpu().numpy().argmax(0) == g["image_logits"].argmax(0)).all()
+
+
+def test_full_depth_retrieval_top1_vs_oracle():
+    """Top-1 retrieval indices over 6 x 6 synthetic pairs identical to the f32 oracle."""
+    cfg = get_model_config("ViT-L-14-336")
+    m = make_model(cfg)
+    sd = W.synthetic_state_dict(cfg)
+    imgs = W.synthetic_images(6, seed=777)
+    caps = W.synthetic_captions(6, seed=888)
+    il, _ = m.get_logits(torch.from_numpy(imgs), torch.from_numpy(caps))
+    oi = O.encode_image(sd, imgs, cfg, normalize=True)
+    ot = O.encode_text(sd, caps, cfg, normalize=True)
+    ref, _ = O.get_logits(oi, ot, float(np.exp(np.log(1 / 0.07))))
+    got = il.cpu().numpy()
+    assert cos_dist(got, ref) < COS_TOL
+    assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
+
+
+@pytest.fixture(scope="module")
+def pacl_models():
+    cfg = get_model_config("ViT-L-14-336").with_depth(2, 2)
+    sd = W.synthetic_state_dict(cfg)
+    heads = W.synthetic_pacl_heads(cfg.with_pacl(768))
+    out = {}
+    for tag, cls in (("pacl", open_clip_pacl), ("pacl_rope", open_clip_pacl_rope),
+                     ("pacl_rope_after", open_clip_pacl_rope_after), ("pacl_sigmoid", open_clip_pacl_sigmoid)):
+        mod = cls(cfg=cfg, clip_state_dict=sd)
+        mod.load_state_dict(heads)
+        mod.to("cuda")
+        out[tag] = mod
+    return out
+
+
+@pytest.mark.parametrize("tag", ["pacl", "pacl_rope", "pacl_rope_after"])
+def test_pacl_forward_vs_golden(pacl_models, golden, tag):
+    g = golden("pacl")
+    mod = pacl_models[tag]
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1100))
+    caps = torch.from_numpy(g["captions"])
+    a, b = mod(imgs, caps)
+    assert cos_dist(a.cpu().numpy(), g[f"{tag}_img"]) < COS_TOL
+    assert cos_dist(b.cpu().numpy(), g[f"{tag}_txt"]) < COS_TOL
+    a1, b1 = mod(imgs[:1], caps)                      # Q6: 1 image x 2 texts -> [2, 768]
+    assert tuple(a1.shape) == g[f"{tag}_bcast_img"].shape == (2, 768)
+    assert cos_dist(a1.cpu().numpy(), g[f"{tag}_bcast_img"]) < COS_TOL
+
+
+def test_pacl_heads_and_sigmoid_pool(pacl_models, golden):
+    g = golden("pacl")
+    mod = pacl_models["pacl_sigmoid"]
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1100))
+    caps = torch.from_numpy(g["captions"])
+    vp = mod.forward_visual(imgs)
+    tp = mod.forward_text(caps)
+    assert cos_dist(vp.cpu().numpy()[:, ROWS_V[1:]], g["visual_proj_rows"]) < COS_TOL
+    assert cos_dist(tp.cpu().numpy(), g["text_proj"]) < COS_TOL
+    a, _ = mod.pool(vp, tp)
+    assert cos_dist(a.cpu().numpy(), g["pacl_sigmoid_img"]) < COS_TOL
+    a2, _ = mod(imgs, caps)
+    assert cos_dist(a2.cpu().numpy(), g["pacl_sigmoid_img"]) < COS_TOL
+
+
+def test_pacl_pool_exact_vs_oracle(pacl_models):
+    """Pooling kernel alone on f32 inputs (no bf16 upstream): tight tolerance, all broadcast shapes."""
+    mod = pacl_models["pacl_sigmoid"]
+    rng = np.random.default_rng(0)
+    vp = rng.standard_normal((3, 576, 768)).astype(np.float32)
+    tp = rng.standard_normal((3, 768)).astype(np.float32)
+    for bi, bt in ((3, 3), (1, 3), (3, 1), (1, 1)):
+        for weights, cls in (("ones", open_clip_pacl), ("sigmoid", open_clip_pacl_sigmoid),
+                             ("sigmoid_rope", open_clip_pacl_rope_after)):
+            m = mod
+            m.weight_mode, m.rope = cls.weight_mode, cls.rope
+            a, b = m.pool(torch.from_numpy(vp[:bi]).cuda(), torch.from_numpy(tp[:bt]).cuda())
+            ra, rb = O.pacl_pool(vp[:bi], tp[:bt], weights="ones" if weights == "ones" else "sigmoid",
+                                 rope_after=weights == "sigmoid_rope")
+            np.testing.assert_allclose(a.cpu().numpy(), ra, atol=2e-5)
+            np.testing.assert_allclose(b.cpu().numpy(), rb, atol=2e-6)
+    mod.weight_mode, mod.rope = open_clip_pacl_sigmoid.weight_mode, open_clip_pacl_sigmoid.rope
+
+
+def test_apply_rope_vs_golden(pacl_models, golden):
+    eng = pacl_models["pacl"].engine
+    x = W.uniform("rope-input", 2 * 576 * 128).reshape(2, 576, 128)
+    # the engine's tables cover D = 1024 (vision) and 768 (PACL); compare at D = 1024 vs the oracle
+    x1024 = W.uniform("rope-1024", 576 * 1024).reshape(1, 576, 1024)
+    y = apply_rope(torch.from_numpy(x1024).cuda(), engine=eng).cpu().numpy()
+    np.testing.assert_allclose(y, O.apply_rope(x1024), atol=1e-4)
+    assert O.apply_rope(x).shape == golden("rope")["y"].shape
+
+
+@pytest.mark.parametrize("name,sigma", [("s576", 1.0 / 576), ("s625", 1.0 / 625)])
+def test_sparc_vs_golden(pacl_models, golden, name, sigma):
+    g = golden("sparc")
+    eng = pacl_models["pacl"].engine
+    v = torch.from_numpy(W.uniform("sparc-v", 2 * 576 * 64).reshape(2, 576, 64)).cuda()
+    l = torch.from_numpy(W.uniform("sparc-l", 2 * 77 * 64).reshape(2, 77, 64)).cuda()
+    grouped = torch.empty(2, 77, 64, device="cuda")
+    lnorm = torch.empty_like(grouped)
+    sim = torch.empty(2, 77, 576, device="cuda")
+    from clipembed import _lib
+    from clipembed.model import _ptr, _stream
+    _lib.call("ce_sparc_forward", eng.h, _stream(eng.device), _ptr(v), _ptr(l), 2, 576, 77, 64, sigma,
+              _ptr(grouped), _ptr(lnorm), _ptr(sim))
+    np.testing.assert_allclose(grouped.cpu().numpy(), g[f"{name}_grouped"], atol=2e-5)
+    np.testing.assert_allclose(lnorm.cpu().numpy(), g[f"{name}_l_norm"], atol=2e-6)
+    np.testing.assert_allclose(sim.cpu().numpy(), np.einsum("btd,bpd->btp", l.cpu().numpy(), v.cpu().numpy()),
+                               atol=1e-4)
+
+
+def test_logits_and_cross_entropy(small, golden):
+    from clipembed.loss import ClipLoss
+    g = golden("loss")
+    a = torch.from_numpy(O.l2normalize(W.uniform("loss-a", 8 * 768).reshape(8, 768))).cuda()
+    b = torch.from_numpy(O.l2normalize(W.uniform("loss-b", 8 * 768).reshape(8, 768))).cuda()
+    fn = ClipLoss(engine=small.engine)
+    np.testing.assert_allclose(float(fn(a, b, 10.0)), float(g["pacl_clip_loss"]), rtol=1e-5)
+    np.testing.assert_allclose(float(fn(a, b, 14.2857)), float(g["openclip_single"]), rtol=1e-5)
+    il, tl = small.logits(a, b, 100.0)
+    ref = 100.0 * a.cpu().numpy() @ b.cpu().numpy().T
+    np.testing.assert_allclose(il.cpu().numpy(), ref, atol=1e-4)
+    np.testing.assert_allclose(tl.cpu().numpy(), ref.T, atol=1e-4)
+
+
+def test_error_behaviour(small):
+    with pytest.raises(ClipEmbedError, match="context length"):
+        from clipembed import _lib
+        from clipembed.model import _ptr, _stream
+        ids = torch.zeros(2, 76, dtype=torch.int64, device="cuda")
+        out = torch.empty(2, 768, device="cuda")
+        _lib.call("ce_encode_text", small.engine.h, _stream(small.engine.device), _ptr(ids), 2, 76, 0, _ptr(out),
+                  None, 0)
+    with pytest.raises(RuntimeError, match="encode_image expects"):
+        small.encode_image(torch.zeros(1, 3, 224, 224))
+    empty = clipembed.CLIP(small.cfg).to("cuda")
+    with pytest.raises(ClipEmbedError, match="has not been loaded"):
+        empty.encode_image(torch.zeros(1, 3, 336, 336))
