@@ -83,6 +83,7 @@ _SIGNATURES = {
                                 POINTER(c_double), POINTER(c_double)]),
     "ce_kernel_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                     c_void_p, c_int]),
+    "ce_set_gemm_schedule": (c_int, [c_int]),
     "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
     "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
 }

@@ -1036,6 +1036,8 @@ int ce_kernel_gemm_bf16(void* stream, const void* A, const void* Wt, int M, int 
     return check_launch(ce::launch_gemm(p, act, out_dtype == CE_BF16, (hipStream_t)stream), "gemm");
 }
 
+int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
+
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal) {
     if (!qkv || !out) return fail(CE_ERR_INVALID, "ce_kernel_attention: null argument");
     if (B <= 0 || L <= 0 || H <= 0) return fail(CE_ERR_INVALID, "ce_kernel_attention: bad sizes");

@@ -40,8 +40,20 @@ __device__ __forceinline__ float wave_min(float v) {
     return v;
 }
 
-// Exact-erf GELU (torch.nn.GELU default) and QuickGELU (transformer.py:32-35).
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7): one exp + one reciprocal, branch-free.
+__device__ __forceinline__ float erf_fast(float x) {
+    const float a = fabsf(x);
+    const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    p *= t;
+    const float y = fmaf(-p, __expf(-a * a), 1.0f);
+    return copysignf(y, x);
+}
+// Exact-erf GELU (torch.nn.GELU default; erf to 1.5e-7) and QuickGELU (transformer.py:32-35).
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
 
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2 };

@@ -23,6 +23,7 @@ struct GemmParams {
     int grp, o_gs, o_go, r_gs, r_go;
 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s);
+int set_gemm_schedule(int v);   // returns previous
 
 // Multi-head attention over a packed QKV activation.
 //   qkv [B*L][3*D] bf16 (q | k | v, head h at columns h*64 .. h*64+63 of each part)

@@ -22,6 +22,8 @@
 #include "ce_device.h"
 #include "ce_kernels.h"
 
+#include <cstdlib>
+
 namespace ce {
 
 namespace {
@@ -45,7 +47,20 @@ __device__ __forceinline__ int map_row(int m, int grp, int gs, int go) {
     return g * gs + go + (m - g * grp);
 }
 
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__device__ __forceinline__ void wait_vm(int n) {
+    // n is a small compile-time constant after inlining/unrolling
+    if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+}
+
+// SCHED 0: 2-stage ring, whole-tile stages, 2 barriers per K-tile (reference schedule).
+// SCHED 1: 4 phases per K-tile; the K-tile is split in half-tiles {A rows of quadrant-row mh,
+//          W rows of quadrant-col nh}, each double-buffered; phase p computes one 64x32
+//          quadrant of every wave's 128x64 output (16 MFMAs) and issues the LDS-DMA of one
+//          half-tile of K-tile t+1, so every load has ~3 phases to land; one barrier per phase.
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
@@ -66,36 +81,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int tn = wgid - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
 
-    // ---- staging addresses: thread -> (row tid>>3 of a 64-row pass, 16-B chunk) ---------
-    const int srow = tid >> 3;
-    const int schunk = (tid & 7) ^ ((tid >> 4) & 7);   // inverse of the LDS swizzle
-    const bf16_t* a_src[4];
-    const bf16_t* w_src[4];
-#pragma unroll
-    for (int ps = 0; ps < 4; ++ps) {
-        int ar = min(m0 + ps * 64 + srow, p.M - 1);
-        int wr = min(n0 + ps * 64 + srow, p.N - 1);
-        a_src[ps] = p.A + (size_t)ar * p.lda + schunk * 8;
-        w_src[ps] = p.W + (size_t)wr * p.ldw + schunk * 8;
-    }
-    const int lds_wave_off = wave * 1024;
-
-    auto stage = [&](int kt, int buf) {
-        char* base = smem + buf * STAGE_BYTES + lds_wave_off;
-        const int koff = kt * BK;
-#pragma unroll
-        for (int ps = 0; ps < 4; ++ps) glds16(a_src[ps] + koff, base + ps * 8192);
-#pragma unroll
-        for (int ps = 0; ps < 4; ++ps) glds16(w_src[ps] + koff, base + TILE_BYTES + ps * 8192);
-    };
-
-    // ---- fragment read offsets (per lane, per k-step) ----------------------------------
     const int fr = lane & 15;
     const int fq = lane >> 4;
     const int frag_off0 = fr * 128 + ((((0 * 4) + fq) ^ (fr >> 1)) << 4);
     const int frag_off1 = fr * 128 + ((((1 * 4) + fq) ^ (fr >> 1)) << 4);
-    const int a_off = wm * 128 * 128;
-    const int w_off = TILE_BYTES + wn * 64 * 128;
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -104,34 +93,168 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = p.K / BK;
-    stage(0, 0);
-    if (nk > 1) stage(1, 1);
 
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier();
-        const char* sb = smem + (kt & 1) * STAGE_BYTES;
+    if constexpr (SCHED == 0) {
+        // ---- staging addresses: thread -> (row tid>>3 of a 64-row pass, 16-B chunk) -----
+        const int srow = tid >> 3;
+        const int schunk = (tid & 7) ^ ((tid >> 4) & 7);   // inverse of the LDS swizzle
+        const bf16_t* a_src[4];
+        const bf16_t* w_src[4];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int fo = ks ? frag_off1 : frag_off0;
-            bf16x8 af[8], wf[4];
+        for (int ps = 0; ps < 4; ++ps) {
+            int ar = min(m0 + ps * 64 + srow, p.M - 1);
+            int wr = min(n0 + ps * 64 + srow, p.N - 1);
+            a_src[ps] = p.A + (size_t)ar * p.lda + schunk * 8;
+            w_src[ps] = p.W + (size_t)wr * p.ldw + schunk * 8;
+        }
+        const int lds_wave_off = wave * 1024;
+        auto stage = [&](int kt, int buf) {
+            char* base = smem + buf * STAGE_BYTES + lds_wave_off;
+            const int koff = kt * BK;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                af[i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 128 + fo);
+            for (int ps = 0; ps < 4; ++ps) glds16(a_src[ps] + koff, base + ps * 8192);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                wf[j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 128 + fo);
+            for (int ps = 0; ps < 4; ++ps) glds16(w_src[ps] + koff, base + TILE_BYTES + ps * 8192);
+        };
+        const int a_off = wm * 128 * 128;
+        const int w_off = TILE_BYTES + wn * 64 * 128;
+        stage(0, 0);
+        if (nk > 1) stage(1, 1);
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+            const char* sb = smem + (kt & 1) * STAGE_BYTES;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int ks = 0; ks < 2; ++ks) {
+                const int fo = ks ? frag_off1 : frag_off0;
+                bf16x8 af[8], wf[4];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 128 + fo);
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+                    wf[j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 128 + fo);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+            }
+            // every wave's fragment reads of this buffer must have landed before it is restaged
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier();
+            if (kt + 2 < nk) stage(kt + 2, kt & 1);
         }
-        // every wave's fragment reads of this buffer must have landed before it is restaged
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+        // ---- half-tile staging ---------------------------------------------------------------
+        // LDS per buffer: A image rows 0..255 (32 KB) then W image rows 0..255 (32 KB), 128-B rows,
+        // chunk c of row r at c ^ ((r>>1)&7).  Half-tile HA[mh] = A rows {mh*64 + j*128 + 0..63},
+        // HB[nh] = W rows {g*64 + nh*32 + 0..31 : g = 0..3}; each is 128 rows = 2 glds per thread.
+        const int rr = tid >> 3;                       // 0..63 row within a 64-row pass
+        const int ca = (tid & 7) ^ ((rr >> 1) & 7);    // source chunk (rows here are ==rr mod 16)
+        // A rows for (mh, j): mh*64 + j*128 + rr ; W rows for (nh, j): (j*2 + (rr>>5))*64 + nh*32 + (rr&31)
+        const bf16_t* a_src[2][2];
+        const bf16_t* w_src[2][2];
+        int a_lds[2][2], w_lds[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int arow = h * 64 + j * 128 + rr;
+                const int wrow = (j * 2 + (rr >> 5)) * 64 + h * 32 + (rr & 31);
+                a_src[h][j] = p.A + (size_t)min(m0 + arow, p.M - 1) * p.lda + ca * 8;
+                w_src[h][j] = p.W + (size_t)min(n0 + wrow, p.N - 1) * p.ldw + ((tid & 7) ^ ((wrow >> 1) & 7)) * 8;
+                // wave-uniform LDS destination of this wave's 8 rows
+                const int arow_w = h * 64 + j * 128 + wave * 8;
+                const int wrow_w = (j * 2 + ((wave * 8) >> 5)) * 64 + h * 32 + ((wave * 8) & 31);
+                a_lds[h][j] = arow_w * 128;
+                w_lds[h][j] = TILE_BYTES + wrow_w * 128;
+            }
+        auto stageA = [&](int kt, int buf, int h) {
+            char* base = smem + buf * STAGE_BYTES;
+            const int koff = kt * BK;
+            glds16(a_src[h][0] + koff, base + a_lds[h][0]);
+            glds16(a_src[h][1] + koff, base + a_lds[h][1]);
+        };
+        auto stageB = [&](int kt, int buf, int h) {
+            char* base = smem + buf * STAGE_BYTES;
+            const int koff = kt * BK;
+            glds16(w_src[h][0] + koff, base + w_lds[h][0]);
+            glds16(w_src[h][1] + koff, base + w_lds[h][1]);
+        };
+        const int a_off = wm * 128 * 128;
+        const int w_off = TILE_BYTES + wn * 64 * 128;
+
+        // prologue: K-tile 0, issue order A0, B0, B1, A1 (same as the steady-state phases)
+        stageA(0, 0, 0);
+        stageB(0, 0, 0);
+        stageB(0, 0, 1);
+        stageA(0, 0, 1);
+        if (nk > 1) wait_vm(4); else wait_vm(0);
         barrier();
-        if (kt + 2 < nk) stage(kt + 2, kt & 1);
+
+        bf16x8 af[4][2], bfr[2][2];
+        auto readA = [&](const char* sb, int mh) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                af[i][0] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off0);
+                af[i][1] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off1);
+            }
+        };
+        auto readB = [&](const char* sb, int nh) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                bfr[j][0] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off0);
+                bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
+            }
+        };
+        auto mfma_q = [&](int mh, int nh) {
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        };
+
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1, nxt = cur ^ 1;
+            const bool more = kt + 1 < nk;
+            const char* sb = smem + cur * STAGE_BYTES;
+            // phase 1: quadrant (0,0); prefetch HA0(t+1)
+            readA(sb, 0);
+            readB(sb, 0);
+            if (more) stageA(kt + 1, nxt, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(0, 0);
+            wait_vm(more ? 4 : 0);        // HB1(t) landed
+            barrier();
+            // phase 2: quadrant (0,1); prefetch HB0(t+1)
+            readB(sb, 1);
+            if (more) stageB(kt + 1, nxt, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(0, 1);
+            wait_vm(more ? 4 : 0);        // HA1(t) landed
+            barrier();
+            // phase 3: quadrant (1,1); prefetch HB1(t+1)
+            readA(sb, 1);
+            if (more) stageB(kt + 1, nxt, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(1, 1);
+            barrier();
+            // phase 4: quadrant (1,0); prefetch HA1(t+1)
+            readB(sb, 0);
+            if (more) stageA(kt + 1, nxt, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(1, 0);
+            wait_vm(more ? 4 : 0);        // HA0(t+1), HB0(t+1) landed
+            barrier();
+        }
     }
 
     // ---- epilogue: lane holds C[m = lane&15][n = 4*(lane>>4) .. +3] of each 16x16 tile ---
@@ -170,14 +293,32 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     }
 }
 
+int g_sched = -1;
+int gemm_sched() {
+    if (g_sched < 0) {
+        const char* e = getenv("CE_GEMM_SCHED");
+        g_sched = (e && *e == '0') ? 0 : 1;
+    }
+    return g_sched;
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    if (gemm_sched() == 0)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     return hipGetLastError();
 }
 
 }  // namespace
+
+int set_gemm_schedule(int v) {
+    const int prev = gemm_sched();
+    g_sched = v ? 1 : 0;
+    return prev;
+}
 
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s) {
     if (p.M <= 0 || p.N <= 0) return hipSuccess;

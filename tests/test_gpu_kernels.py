@@ -36,7 +36,9 @@ def gemm_ref(A, W, bias, act, resid):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 1024), (4617, 3072, 1024), (1154, 1024, 4096),
                                    (231, 2304, 768), (5, 768, 1024), (700, 832, 640), (1, 64, 64)])
 @pytest.mark.parametrize("variant", ["bias_bf16", "gelu_bf16", "qgelu_bf16", "resid_f32", "plain_f32"])
-def test_gemm(M, N, K, variant):
+@pytest.mark.parametrize("sched", [1, 0])
+def test_gemm(M, N, K, variant, sched):
+    prev = _lib.lib().ce_set_gemm_schedule(sched)
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
     A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
@@ -48,6 +50,7 @@ def test_gemm(M, N, K, variant):
     _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), act, P(resid), P(out),
               _lib.CE_BF16 if out_bf16 else _lib.CE_F32)
     torch.cuda.synchronize()
+    _lib.lib().ce_set_gemm_schedule(prev)
     ref = gemm_ref(A, W, bias, act, resid)
     err = (out.float() - ref).abs().max().item()
     scale = ref.abs().max().item()

@@ -1,0 +1,94 @@
+"""Kernel micro-benchmarks at the ViT-L/14-336 bench shapes (B = 256 per GPU), random data,
+interleaved A/B of GEMM schedules in one process (guide §5.4 rule 24).
+
+    python tools/bench_kernels.py [--batch 256] [--reps 10] [--rounds 3]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "clip-embeds_amd"), REPO]
+
+import torch  # noqa: E402
+
+from clipembed import _lib  # noqa: E402
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def timeit(fn, reps):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--scheds", default="0,1")
+    args = ap.parse_args()
+    B = args.batch
+    Mv, Mt = B * 577, B * 77
+    shapes = {  # name: (M, N, K, act, resid, out_bf16)
+        "qkv_v": (Mv, 3072, 1024, 0, False, True), "out_v": (Mv, 1024, 1024, 0, True, False),
+        "fc_v": (Mv, 4096, 1024, 1, False, True), "proj_v": (Mv, 1024, 4096, 0, True, False),
+        "qkv_t": (Mt, 2304, 768, 0, False, True), "fc_t": (Mt, 3072, 768, 1, False, True),
+    }
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    res = {}
+    bufs = {}
+    for name, (M, N, K, act, resid, ob) in shapes.items():
+        A = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+        W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+        bias = torch.rand(N, device="cuda", generator=g)
+        R = torch.rand(M, N, device="cuda", generator=g) if resid else None
+        O = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
+        bufs[name] = (A, W, bias, R, O)
+    for rnd in range(args.rounds):
+        for sched in [int(x) for x in args.scheds.split(",")]:
+            _lib.lib().ce_set_gemm_schedule(sched)
+            for name, (M, N, K, act, resid, ob) in shapes.items():
+                A, W, bias, R, O = bufs[name]
+
+                def fn():
+                    _lib.call("ce_kernel_gemm_bf16", stream, P(A), P(W), M, N, K, P(bias), act, P(R), P(O),
+                              _lib.CE_BF16 if ob else _lib.CE_F32)
+                ms = timeit(fn, args.reps)
+                tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
+                res.setdefault(f"{name}/s{sched}", []).append(tf)
+    for attn, (L, H, causal, Bx) in {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B)}.items():
+        qkv = (torch.randn(Bx * L, 3 * H * 64, device="cuda", generator=g)).to(torch.bfloat16)
+        out = torch.empty(Bx * L, H * 64, device="cuda", dtype=torch.bfloat16)
+        for rnd in range(args.rounds):
+            ms = timeit(lambda: _lib.call("ce_kernel_attention", stream, P(qkv), P(out), Bx, L, H, causal), args.reps)
+            res.setdefault(attn, []).append(4.0 * Bx * H * L * L * 64 / (ms * 1e-3) / 1e12)
+    for rows, D in ((Mv, 1024),):
+        x = torch.randn(rows, D, device="cuda", generator=g)
+        w = torch.ones(D, device="cuda")
+        o = torch.empty(rows, D, device="cuda", dtype=torch.bfloat16)
+        for rnd in range(args.rounds):
+            ms = timeit(lambda: _lib.call("ce_kernel_layernorm", stream, P(x), P(o), _lib.CE_BF16, P(w), P(w), rows, D),
+                        args.reps)
+            res.setdefault("ln_v (GB/s)", []).append(rows * D * 6 / (ms * 1e-3) / 1e9)
+    for k, v in res.items():
+        print(f"{k:<16} " + " ".join(f"{x:8.1f}" for x in v) + f"   best {max(v):8.1f}")
+    print(json.dumps({k: round(max(v), 1) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
