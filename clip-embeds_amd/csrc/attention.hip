@@ -48,7 +48,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                                                     float scale_log2) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
-    const int b = blockIdx.z, h = blockIdx.y, qb = blockIdx.x;
+    // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
+    // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
+    const int nqb = (L + QBLK - 1) / QBLK;
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
+    const int wgid = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    const int bh = wgid / nqb;
+    const int qb = wgid - bh * nqb;
+    const int b = bh / H, h = bh - b * H;
     const int D = H * 64;
     const long ld = 3L * D;
     const bf16_t* base = qkv + (size_t)b * L * ld;
@@ -59,6 +68,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int r = lane & 31;
     const int h2 = lane >> 5;
     const int qrow = qb * QBLK + wave * 32 + r;
+    const int q_wave0 = qb * QBLK + wave * 32;        // first query of this wave (wave-uniform)
 
     // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
     bf16x8 qf[4];
@@ -72,6 +82,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int srow = tid >> 3;
     const int spos = tid & 7;
     const int kchunk = spos ^ ((tid >> 4) & 7);
+    const int vchunk = spos ^ (((srow >> 1) & 1) << 2);   // V image swizzle (conflict-free tr reads)
     const int kv_end = CAUSAL ? min(L, qb * QBLK + QBLK) : L;
     const int nkt = (kv_end + KBLK - 1) / KBLK;
     const bf16_t* kbase = base + D + h * 64;
@@ -83,7 +94,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         for (int ps = 0; ps < 2; ++ps) {
             const int key = min(t * KBLK + ps * 32 + srow, L - 1);
             glds16(kbase + (size_t)key * ld + kchunk * 8, dst + ps * 4096);
-            glds16(vbase + (size_t)key * ld + spos * 8, dst + TILE_KV_BYTES + ps * 4096);
+            glds16(vbase + (size_t)key * ld + vchunk * 8, dst + TILE_KV_BYTES + ps * 4096);
         }
     };
 
@@ -96,10 +107,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             const int row = kt2 * 32 + r;
             koff[kt2][ks] = row * 128 + (((2 * ks + h2) ^ ((row >> 1) & 7)) << 4);
         }
-    // V^T via ds_read_b64_tr_b16: 16-lane group G supplies rows (keys) kb + 4*(G>>1) + (i>>2),
-    // columns dt*32 + 16*(G&1) + 4*(i&3)
+    // V^T via ds_read_b64_tr_b16: 16-lane group G supplies rows (keys) kb + 4*(G>>1) + q,
+    // columns dt*32 + 16*(G&1) + 4*p (q = i>>2, p = i&3); the 16-B chunk of that address is
+    // XOR-ed with 4*((row>>1)&1) = 4*((q>>1)&1) (rows kb + 4*(G>>1) are multiples of 4).
     const int G = lane >> 4, gi = lane & 15;
-    const int voff_lane = (4 * (G >> 1) + (gi >> 2)) * 128 + (16 * (G & 1) + 4 * (gi & 3)) * 2;
+    const int vq = gi >> 2, vp = gi & 3;
+    int voff[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int chunk = dt * 4 + 2 * (G & 1) + (vp >> 1);
+        voff[dt] = (4 * (G >> 1) + vq) * 128 + ((chunk ^ (((vq >> 1) & 1) << 2)) << 4) + (vp & 1) * 8;
+    }
 
     f32x16 o[2];
 #pragma unroll
@@ -119,70 +137,84 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         const char* kb = smem + (t & 1) * STAGE_BYTES;
         const char* vb = kb + TILE_KV_BYTES;
 
-        // ---- S^T = K Q^T (two 32-key subtiles) ----
-        f32x16 s[2];
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
-                s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
+        // waves whose queries are all padding, or (causal) whose queries all precede this key
+        // tile, skip the math but keep the workgroup barriers
+        const bool active = q_wave0 < L && !(CAUSAL && t * KBLK > q_wave0 + 31);
+        if (active) {
+            // ---- S^T = K Q^T (two 32-key subtiles) ----
+            f32x16 s[2];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2) {
+    #pragma unroll
+                for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+    #pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                    s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
+                }
             }
+
+            // ---- online softmax (log2 domain, scale folded into one FMA per score) ----
+            const int key0 = t * KBLK;
+            // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
+            const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
+            if (need_mask) {
+    #pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
+                        const bool masked = (key >= L) || (CAUSAL && key > qrow);
+                        s[kt2][i] = masked ? -INFINITY : s[kt2][i];
+                    }
+            }
+            float tmax = s[0][0];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax = fmaxf(tmax, s[kt2][i]);
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+            const float m_new = fmaxf(m_run, tmax);
+            if (__any(m_new > m_run)) {      // wave-uniform: rescale only when some row max grew
+                const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+                m_run = m_new;
+                l_run *= alpha;
+    #pragma unroll
+                for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+            }
+            const float mc = m_run * scale_log2;
+            float psum = 0.f;
+            bf16x8 pf[2][2];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float pv = __builtin_amdgcn_exp2f(fmaf(s[kt2][8 * s2 + j], scale_log2, -mc));
+                        psum += pv;
+                        pf[kt2][s2][j] = (__bf16)pv;
+                    }
+            l_run += psum;
+
+            // ---- O^T += V^T P^T ----
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int krow = kt2 * 32 + 16 * s2;
+    #pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) {
+                        const char* a0 = vb + krow * 128 + voff[dt];
+                        const s16x4 lo = ds_read_tr16(a0);
+                        const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
+                        typedef __attribute__((ext_vector_type(8))) short s16x8;
+                        const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                        const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
+                    }
+                }
         }
-
-        // ---- online softmax (log2 domain) ----
-        const int key0 = t * KBLK;
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
-                float x = s[kt2][i] * scale_log2;
-                const bool masked = (key >= L) || (CAUSAL && key > qrow);
-                x = masked ? -INFINITY : x;
-                s[kt2][i] = x;
-                tmax = fmaxf(tmax, x);
-            }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float m_new = fmaxf(m_run, tmax);
-        const float alpha = exp2f(m_run - m_new);
-        m_run = m_new;
-        float psum = 0.f;
-        bf16x8 pf[2][2];
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float pv = exp2f(s[kt2][8 * s2 + j] - m_new);
-                    psum += pv;
-                    pf[kt2][s2][j] = (__bf16)pv;
-                }
-        l_run = l_run * alpha + psum;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-
-        // ---- O^T += V^T P^T ----
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int krow = kt2 * 32 + 16 * s2;
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const char* a0 = vb + krow * 128 + dt * 64 + voff_lane;
-                    const s16x4 lo = ds_read_tr16(a0);
-                    const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
-                    typedef __attribute__((ext_vector_type(8))) short s16x8;
-                    const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                    const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
-                }
-            }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier();
     }
@@ -210,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal,
                             hipStream_t s) {
     if (B <= 0 || L <= 0) return hipSuccess;
-    const dim3 grid((L + QBLK - 1) / QBLK, H, B);
+    const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float scale_log2 = 0.125f * 1.4426950408889634f;   // 1/sqrt(64) * log2(e)
     if (causal)
         hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, scale_log2);

@@ -55,6 +55,351 @@ __device__ __forceinline__ void wait_vm(int n) {
     else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
 }
 
+template <bool ON>
+__device__ __forceinline__ void wait_vm_if(int n) {
+    if constexpr (ON) wait_vm(n);
+}
+template <bool ON>
+__device__ __forceinline__ void barrier_if() {
+    if constexpr (ON) barrier();
+}
+
+// Epilogue: lane holds C[m = mbase + 16i + (lane&15)][n = nbase + 16j + 4(lane>>4) .. +3].
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase, int nbase,
+                                              int lane) {
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = mbase + i * 16 + fr;
+        if (m >= p.M) continue;
+        const int orow = map_row(m, p.grp, p.o_gs, p.o_go);
+        int rrow = 0;
+        if constexpr (HAS_RESID) rrow = map_row(m, p.grp, p.r_gs, p.r_go);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = nbase + j * 16 + fq * 4;
+            if (n >= p.N) continue;
+            f32x4 v = acc[i][j];
+            if (p.bias) {
+                const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+            }
+            v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
+            v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
+            if constexpr (HAS_RESID) {
+                const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)rrow * p.ldr + n);
+                v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+            }
+            if constexpr (OUT_BF16) {
+                uint2 o;
+                o.x = pack_bf2(v[0], v[1]);
+                o.y = pack_bf2(v[2], v[3]);
+                *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + (size_t)orow * p.ldo + n) = o;
+            } else {
+                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)orow * p.ldo + n) =
+                    make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
+// Buffer descriptor from provably wave-uniform inputs: without the readfirstlanes hipcc keeps the
+// words in VGPRs and wraps every buffer op in a waterfall loop (guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int nbytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const int n = __builtin_amdgcn_readfirstlane(nbytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n,
+                                             0x00020000);
+}
+
+// Bijective XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous range
+// of tile ids so the tiles that share A / W panels run on one L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// ------------------------------------------------------------------------------------------
+// SCHED 6 ("early"): 2 whole-K-tile LDS buffers (BK = 64, 128 KB); all 8 LDS-DMA loads of
+// K-tile t+1 are issued at the start of K-tile t (its buffer was released by the previous
+// barrier), so they have a full K-tile of MFMA work (64 per wave) to land.  Inside a K-tile
+// there are no barriers: each wave walks its four 64x32 output quadrants (fragments read per
+// quadrant, 16 MFMAs each) and the two waves of a SIMD drift, overlapping one's LDS reads with
+// the other's MFMAs.  One vmcnt(0) + barrier per K-tile.  LDS image as SCHED 1 (128-B rows,
+// chunk c of row r at c ^ ((r>>1)&7)); staging by buffer_load ... lds descriptors.
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_early(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int nwg = ((p.M + BM - 1) / BM) * tiles_n;
+    const int wgid = xcd_remap(blockIdx.x, nwg);
+    const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // staging: thread -> row (tid>>3) + 64*j (j = 0..3), 16-B chunk (tid&7); per wave-instruction
+    // 8 rows x 128 B = 1 KB lane-linear
+    const int srow = tid >> 3;
+    const int schunk = (tid & 7) ^ ((srow >> 1) & 7);
+    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
+    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
+    __amdgpu_buffer_rsrc_t srdA[4], srdW[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ab = m0 + j * 64, wb = n0 + j * 64;
+        const int arows = max(0, min(p.M - ab, 64)), wrows = max(0, min(p.N - wb, 64));
+        srdA[j] = make_srd(p.A + (size_t)min(ab, p.M - 1) * p.lda, arows * (int)p.lda * 2);
+        srdW[j] = make_srd(p.W + (size_t)min(wb, p.N - 1) * p.ldw, wrows * (int)p.ldw * 2);
+    }
+    const int lds_wave = wave * 1024;
+    auto stage = [&](int kt, int buf) {
+        char* base = smem + buf * STAGE_BYTES + lds_wave;
+        const int kb = kt * BK * 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA[j], (CE_LDS void*)(base + j * 8192), 16, voffA, kb, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW[j], (CE_LDS void*)(base + TILE_BYTES + j * 8192), 16, voffW,
+                                                     kb, 0, 0);
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int frag_off0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
+    const int frag_off1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 64 * 128;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 af[4][2], bfr[2][2];
+    auto readA = [&](const char* sb, int mh) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af[i][0] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off0);
+            af[i][1] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off1);
+        }
+    };
+    auto readB = [&](const char* sb, int nh) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            bfr[j][0] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off0);
+            bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
+        }
+    };
+    auto mfma_q = [&](int mh, int nh) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    };
+
+    const int nk = p.K / BK;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const char* sb = smem + cur * STAGE_BYTES;
+        if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+        readA(sb, 0);
+        readB(sb, 0);
+        mfma_q(0, 0);
+        readB(sb, 1);
+        mfma_q(0, 1);
+        readA(sb, 1);
+        mfma_q(1, 1);
+        readB(sb, 0);
+        mfma_q(1, 0);
+        if (kt + 1 < nk) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // K-tile t+1 landed; reads done
+            barrier();                                          // everyone's; buffer cur released
+        }
+    }
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// SCHED 9 ("persistent"): SCHED 1's 4-phase half-tile pipeline run as ONE continuous K-step
+// stream over all the tiles a workgroup owns.  Grid = one 512-thread workgroup per CU; the
+// workgroups of XCD x own a contiguous range of tile ids (stride 32 inside it).  During the last
+// K-step of tile i the half-tiles of tile i+1's first K-step are issued (same buffer parity
+// rules as inside a tile), so the next tile's loads land while tile i's epilogue runs, and the
+// epilogue's stores drain while tile i+1 computes.  Per tile the epilogue starts with
+// vmcnt(0) + barrier (tile i+1's step-0 half-tiles then are landed and visible), which lets the
+// first two waits of the next tile be skipped (they would otherwise wait for the stores).
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_persist(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int T = ((p.M + BM - 1) / BM) * tiles_n;
+    const int W8 = gridDim.x >> 3;                 // workgroups per XCD group (grid % 8 == 0)
+    const int xcd = blockIdx.x & 7;
+    const int q8 = T >> 3, r8 = T & 7;
+    const int xs = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+    const int xe = xs + q8 + (xcd < r8 ? 1 : 0);
+    const int first = xs + (blockIdx.x >> 3);
+    if (first >= xe) return;
+
+    // staging geometry (as SCHED 1 / 2): half-tile HA[h] = A rows h*64 + j*128 + rr, HB[h] = W rows
+    // (2j + (rr>>5))*64 + h*32 + (rr&31), j = 0..1, rr = tid>>3; chunk swizzle c ^ ((r>>1)&7)
+    const int rr = tid >> 3;
+    const int chunk = (tid & 7) ^ ((rr >> 1) & 7);
+    const int voffA = rr * (int)p.lda * 2 + chunk * 16;
+    const int voffB = ((rr >> 5) * 64 + (rr & 31)) * (int)p.ldw * 2 + chunk * 16;
+    int a_lds[2][2], w_lds[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            a_lds[h][j] = (h * 64 + j * 128 + wave * 8) * 128;
+            w_lds[h][j] = TILE_BYTES + ((j * 2 + ((wave * 8) >> 5)) * 64 + h * 32 + ((wave * 8) & 31)) * 128;
+        }
+    auto stageA = [&](int mt0, int kt, int buf, int h) {
+        char* base = smem + buf * STAGE_BYTES;
+        const int kb = kt * BK * 2;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ab = mt0 + h * 64 + j * 128;
+            const int rows = max(0, min(p.M - ab, 64));
+            const __amdgpu_buffer_rsrc_t srd = make_srd(p.A + (size_t)min(ab, p.M - 1) * p.lda, rows * (int)p.lda * 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (CE_LDS void*)(base + a_lds[h][j]), 16, voffA, kb, 0, 0);
+        }
+    };
+    auto stageB = [&](int nt0, int kt, int buf, int h) {
+        char* base = smem + buf * STAGE_BYTES;
+        const int kb = kt * BK * 2;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int bb = nt0 + j * 128 + h * 32;
+            const int rows = max(0, min(p.N - bb, 96));
+            const __amdgpu_buffer_rsrc_t srd = make_srd(p.W + (size_t)min(bb, p.N - 1) * p.ldw, rows * (int)p.ldw * 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (CE_LDS void*)(base + w_lds[h][j]), 16, voffB, kb, 0, 0);
+        }
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int frag_off0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
+    const int frag_off1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 64 * 128;
+    bf16x8 af[4][2], bfr[2][2];
+    f32x4 acc[8][4];
+    auto readA = [&](const char* sb, int mh) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af[i][0] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off0);
+            af[i][1] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off1);
+        }
+    };
+    auto readB = [&](const char* sb, int nh) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            bfr[j][0] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off0);
+            bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
+        }
+    };
+    auto mfma_q = [&](int mh, int nh) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    const int nk = p.K / BK;
+    int tm = first / tiles_n;
+    int m0 = tm * BM, n0 = (first - tm * tiles_n) * BN;
+    // prologue: step 0 of the first tile, issue order A0, B0, B1, A1
+    stageA(m0, 0, 0, 0);
+    stageB(n0, 0, 0, 0);
+    stageB(n0, 0, 0, 1);
+    stageA(m0, 0, 0, 1);
+    wait_vm(4);
+    barrier();
+    int par = 0;                                   // buffer parity of the current K-step
+    for (int t = first; t < xe; t += W8) {
+        const bool has_next = t + W8 < xe;
+        int m0n = 0, n0n = 0;
+        if (has_next) {
+            const int tmn = (t + W8) / tiles_n;
+            m0n = tmn * BM;
+            n0n = (t + W8 - tmn * tiles_n) * BN;
+        }
+        const bool fresh = t != first;             // step-0 half-tiles already waited in the epilogue
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = par, nxt = par ^ 1;
+            const bool more = kt + 1 < nk;
+            const bool load = more || has_next;
+            const int lm = more ? m0 : m0n, ln = more ? n0 : n0n, lk = more ? kt + 1 : 0;
+            const bool skipw = fresh && kt == 0;
+            const char* sb = smem + cur * STAGE_BYTES;
+            // phase 1: quadrant (0,0); prefetch HA0(next step)
+            readA(sb, 0);
+            readB(sb, 0);
+            if (load) stageA(lm, lk, nxt, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(0, 0);
+            if (!skipw) wait_vm(load ? 4 : 0);     // HB1(this step)
+            barrier();
+            // phase 2: quadrant (0,1); prefetch HB0(next)
+            readB(sb, 1);
+            if (load) stageB(ln, lk, nxt, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(0, 1);
+            if (!skipw) wait_vm(load ? 4 : 0);     // HA1(this step)
+            barrier();
+            // phase 3: quadrant (1,1); prefetch HB1(next)
+            readA(sb, 1);
+            if (load) stageB(ln, lk, nxt, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(1, 1);
+            barrier();
+            // phase 4: quadrant (1,0); prefetch HA1(next)
+            readB(sb, 0);
+            if (load) stageA(lm, lk, nxt, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_q(1, 0);
+            wait_vm(load ? 4 : 0);                 // HA0(next), HB0(next)
+            barrier();
+            par = nxt;
+        }
+        // next tile's step-0 half-tiles all landed and visible before the epilogue's traffic
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+        gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+        m0 = m0n;
+        n0 = n0n;
+    }
+}
+
 // SCHED 0: 2-stage ring, whole-tile stages, 2 barriers per K-tile (reference schedule).
 // SCHED 1: 4 phases per K-tile; the K-tile is split in half-tiles {A rows of quadrant-row mh,
 //          W rows of quadrant-col nh}, each double-buffered; phase p computes one 64x32
@@ -146,7 +491,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
             barrier();
             if (kt + 2 < nk) stage(kt + 2, kt & 1);
         }
-    } else {
+    } else if constexpr (SCHED == 1 || SCHED == 3 || SCHED == 4 || SCHED == 7) {
+        // SCHED 3/4/7: timing ablations of SCHED 1 (3: no global loads; 4: no loads, no barriers;
+        // 7: loads issued but never waited for).  Wrong results; micro-benchmark only.
+        constexpr bool LOADS = SCHED == 1 || SCHED == 7;
+        constexpr bool WAITS = SCHED == 1;
+        constexpr bool BARS = SCHED != 4;
         // ---- half-tile staging ---------------------------------------------------------------
         // LDS per buffer: A image rows 0..255 (32 KB) then W image rows 0..255 (32 KB), 128-B rows,
         // chunk c of row r at c ^ ((r>>1)&7).  Half-tile HA[mh] = A rows {mh*64 + j*128 + 0..63},
@@ -172,12 +522,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
                 w_lds[h][j] = TILE_BYTES + wrow_w * 128;
             }
         auto stageA = [&](int kt, int buf, int h) {
+            if constexpr (!LOADS) return;
             char* base = smem + buf * STAGE_BYTES;
             const int koff = kt * BK;
             glds16(a_src[h][0] + koff, base + a_lds[h][0]);
             glds16(a_src[h][1] + koff, base + a_lds[h][1]);
         };
         auto stageB = [&](int kt, int buf, int h) {
+            if constexpr (!LOADS) return;
             char* base = smem + buf * STAGE_BYTES;
             const int koff = kt * BK;
             glds16(w_src[h][0] + koff, base + w_lds[h][0]);
@@ -191,8 +543,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
         stageB(0, 0, 0);
         stageB(0, 0, 1);
         stageA(0, 0, 1);
-        if (nk > 1) wait_vm(4); else wait_vm(0);
-        barrier();
+        if (nk > 1) wait_vm_if<WAITS>(4); else wait_vm_if<WAITS>(0);
+        barrier_if<BARS>();
 
         bf16x8 af[4][2], bfr[2][2];
         auto readA = [&](const char* sb, int mh) {
@@ -209,19 +561,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
                 bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
             }
         };
-        auto mfma_q = [&](int mh, int nh) {
+
+        // MFMAs of one quadrant, optionally split in two halves with `mid` issued in between
+        auto mfma_half = [&](int mh, int nh, int ks) {
             __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+                for (int j = 0; j < 2; ++j)
+                    acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
         };
-
+        auto phase = [&](int mh, int nh, auto&& loads) {
+            loads();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mfma_half(mh, nh, 0);
+            mfma_half(mh, nh, 1);
+        };
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1, nxt = cur ^ 1;
             const bool more = kt + 1 < nk;
@@ -229,84 +586,76 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
             // phase 1: quadrant (0,0); prefetch HA0(t+1)
             readA(sb, 0);
             readB(sb, 0);
-            if (more) stageA(kt + 1, nxt, 0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(0, 0);
-            wait_vm(more ? 4 : 0);        // HB1(t) landed
-            barrier();
+            phase(0, 0, [&] { if (more) stageA(kt + 1, nxt, 0); });
+            wait_vm_if<WAITS>(more ? 4 : 0);        // HB1(t) landed
+            barrier_if<BARS>();
             // phase 2: quadrant (0,1); prefetch HB0(t+1)
             readB(sb, 1);
-            if (more) stageB(kt + 1, nxt, 0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(0, 1);
-            wait_vm(more ? 4 : 0);        // HA1(t) landed
-            barrier();
+            phase(0, 1, [&] { if (more) stageB(kt + 1, nxt, 0); });
+            wait_vm_if<WAITS>(more ? 4 : 0);        // HA1(t) landed
+            barrier_if<BARS>();
             // phase 3: quadrant (1,1); prefetch HB1(t+1)
             readA(sb, 1);
-            if (more) stageB(kt + 1, nxt, 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(1, 1);
-            barrier();
+            phase(1, 1, [&] { if (more) stageB(kt + 1, nxt, 1); });
+            barrier_if<BARS>();
             // phase 4: quadrant (1,0); prefetch HA1(t+1)
             readB(sb, 0);
-            if (more) stageA(kt + 1, nxt, 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(1, 0);
-            wait_vm(more ? 4 : 0);        // HA0(t+1), HB0(t+1) landed
-            barrier();
+            phase(1, 0, [&] { if (more) stageA(kt + 1, nxt, 1); });
+            wait_vm_if<WAITS>(more ? 4 : 0);        // HA0(t+1), HB0(t+1) landed
+            barrier_if<BARS>();
         }
     }
 
-    // ---- epilogue: lane holds C[m = lane&15][n = 4*(lane>>4) .. +3] of each 16x16 tile ---
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wm * 128 + i * 16 + fr;
-        if (m >= p.M) continue;
-        const int orow = map_row(m, p.grp, p.o_gs, p.o_go);
-        int rrow = 0;
-        if constexpr (HAS_RESID) rrow = map_row(m, p.grp, p.r_gs, p.r_go);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + wn * 64 + j * 16 + fq * 4;
-            if (n >= p.N) continue;
-            f32x4 v = acc[i][j];
-            if (p.bias) {
-                const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-            }
-            v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
-            v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
-            if constexpr (HAS_RESID) {
-                const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)rrow * p.ldr + n);
-                v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-            }
-            if constexpr (OUT_BF16) {
-                uint2 o;
-                o.x = pack_bf2(v[0], v[1]);
-                o.y = pack_bf2(v[2], v[3]);
-                *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + (size_t)orow * p.ldo + n) = o;
-            } else {
-                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)orow * p.ldo + n) =
-                    make_float4(v[0], v[1], v[2], v[3]);
-            }
-        }
-    }
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
 }
 
 int g_sched = -1;
 int gemm_sched() {
     if (g_sched < 0) {
         const char* e = getenv("CE_GEMM_SCHED");
-        g_sched = (e && *e == '0') ? 0 : 1;
+        g_sched = e ? atoi(e) : 1;
+        if (!(g_sched == 0 || g_sched == 1 || g_sched == 3 || g_sched == 4 || g_sched == 6 || g_sched == 7 ||
+              g_sched == 9))
+            g_sched = 1;
     }
     return g_sched;
+}
+
+int g_num_cu = 0;
+int num_cus() {
+    if (g_num_cu <= 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            g_num_cu = n;
+        else
+            g_num_cu = 256;
+    }
+    return g_num_cu;
 }
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p, hipStream_t s) {
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    if (gemm_sched() == 0)
+    const int sc = gemm_sched();
+    if (sc == 9) {
+        // one workgroup per CU (a multiple of 8 so every XCD group is complete)
+        int grid = (num_cus() / 8) * 8;
+        const int need = ((nwg + 7) / 8) * 8;
+        grid = grid < need ? grid : need;
+        hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
+    } else if (sc == 0)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (sc == 1)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (sc == 6)
+        hipLaunchKernelGGL((gemm_bf16_early<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 3)   // timing ablations (qkv shape only)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 3>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 4)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 4>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 7)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 7>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     else
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     return hipGetLastError();
@@ -316,7 +665,7 @@ hipError_t launch_t(const GemmParams& p, hipStream_t s) {
 
 int set_gemm_schedule(int v) {
     const int prev = gemm_sched();
-    g_sched = v ? 1 : 0;
+    g_sched = (v == 0 || v == 3 || v == 4 || v == 6 || v == 7 || v == 9) ? v : 1;
     return prev;
 }
 

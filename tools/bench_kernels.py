@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--scheds", default="0,1")
+    ap.add_argument("--only", default="", help="comma list of shape names to run (default all)")
     args = ap.parse_args()
     B = args.batch
     Mv, Mt = B * 577, B * 77
@@ -47,7 +48,12 @@ def main():
         "qkv_v": (Mv, 3072, 1024, 0, False, True), "out_v": (Mv, 1024, 1024, 0, True, False),
         "fc_v": (Mv, 4096, 1024, 1, False, True), "proj_v": (Mv, 1024, 4096, 0, True, False),
         "qkv_t": (Mt, 2304, 768, 0, False, True), "fc_t": (Mt, 3072, 768, 1, False, True),
+        # diagnostics: A resident in L2/MALL (M = 8192) and a square 4096^3 reference point
+        "qkv_m8k": (8192, 3072, 1024, 0, False, True), "sq4096": (4096, 4096, 4096, 0, False, True),
     }
+    if args.only:
+        keep = set(args.only.split(","))
+        shapes = {k: v for k, v in shapes.items() if k in keep}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device="cuda").manual_seed(0)
     res = {}
@@ -71,13 +77,16 @@ def main():
                 ms = timeit(fn, args.reps)
                 tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
                 res.setdefault(f"{name}/s{sched}", []).append(tf)
-    for attn, (L, H, causal, Bx) in {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B)}.items():
+    attns = {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B)}
+    if args.only:
+        attns = {k: v for k, v in attns.items() if k in keep}
+    for attn, (L, H, causal, Bx) in attns.items():
         qkv = (torch.randn(Bx * L, 3 * H * 64, device="cuda", generator=g)).to(torch.bfloat16)
         out = torch.empty(Bx * L, H * 64, device="cuda", dtype=torch.bfloat16)
         for rnd in range(args.rounds):
             ms = timeit(lambda: _lib.call("ce_kernel_attention", stream, P(qkv), P(out), Bx, L, H, causal), args.reps)
             res.setdefault(attn, []).append(4.0 * Bx * H * L * L * 64 / (ms * 1e-3) / 1e12)
-    for rows, D in ((Mv, 1024),):
+    for rows, D in (((Mv, 1024),) if not args.only or "ln_v" in keep else ()):
         x = torch.randn(rows, D, device="cuda", generator=g)
         w = torch.ones(D, device="cuda")
         o = torch.empty(rows, D, device="cuda", dtype=torch.bfloat16)
