@@ -106,7 +106,7 @@ def main():
     _lib.call("ce_reserve", model.engine.h, B, B)
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
-    scale = float(model.logit_scale.exp())
+    scale = float(model.logit_scale.detach().exp())
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s, batch {B}/GPU, world {world}")
 
     def step():

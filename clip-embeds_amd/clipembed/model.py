@@ -253,7 +253,7 @@ class CLIP(torch.nn.Module):
     def get_logits(self, image, text):
         image_features = self._pooled(self.encode_image(image, normalize=True))
         text_features = self._pooled(self.encode_text(text, normalize=True))
-        return self.logits(image_features, text_features, float(self.logit_scale.exp()))
+        return self.logits(image_features, text_features, float(self.logit_scale.detach().exp()))
 
     @staticmethod
     def _pooled(x):

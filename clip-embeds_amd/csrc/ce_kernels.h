@@ -21,6 +21,7 @@ struct GemmParams {
     const float* resid; long ldr;      // nullable, f32
     void* out; long ldo;               // f32 or bf16
     int grp, o_gs, o_go, r_gs, r_go;
+    int gm = 0;                        // tile-order M-group (set by launch_gemm)
 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s);
 int set_gemm_schedule(int v);   // returns previous

@@ -65,45 +65,10 @@ __device__ __forceinline__ void barrier_if() {
 }
 
 // Epilogue: lane holds C[m = mbase + 16i + (lane&15)][n = nbase + 16j + 4(lane>>4) .. +3].
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase, int nbase,
-                                              int lane) {
-    const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = mbase + i * 16 + fr;
-        if (m >= p.M) continue;
-        const int orow = map_row(m, p.grp, p.o_gs, p.o_go);
-        int rrow = 0;
-        if constexpr (HAS_RESID) rrow = map_row(m, p.grp, p.r_gs, p.r_go);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = nbase + j * 16 + fq * 4;
-            if (n >= p.N) continue;
-            f32x4 v = acc[i][j];
-            if (p.bias) {
-                const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-                v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-            }
-            v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
-            v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
-            if constexpr (HAS_RESID) {
-                const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)rrow * p.ldr + n);
-                v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
-            }
-            if constexpr (OUT_BF16) {
-                uint2 o;
-                o.x = pack_bf2(v[0], v[1]);
-                o.y = pack_bf2(v[2], v[3]);
-                *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + (size_t)orow * p.ldo + n) = o;
-            } else {
-                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)orow * p.ldo + n) =
-                    make_float4(v[0], v[1], v[2], v[3]);
-            }
-        }
-    }
-}
-
+// vmcnt counts stores as well as loads and retires in order, so a residual/bias load issued after
+// earlier stores waits for those stores too: bias is loaded once up front and the residual rows of
+// fragment row i+1 are issued before the stores of row i (two-deep register ring), so each store
+// batch has a full row of work to drain behind it.
 // Buffer descriptor from provably wave-uniform inputs: without the readfirstlanes hipcc keeps the
 // words in VGPRs and wraps every buffer op in a waterfall loop (guide T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int nbytes) {
@@ -115,11 +80,105 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int
                                              0x00020000);
 }
 
+template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M>
+__device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase,
+                                                   int nbase, int lane) {
+    const int fr = lane & 15, fq = lane >> 4;
+    // bias through a buffer descriptor: a null bias gets num_records 0 and reads zeros, with no branch
+    const __amdgpu_buffer_rsrc_t bsrd = make_srd(p.bias ? (const void*)p.bias : (const void*)p.A, p.bias ? p.N * 4 : 0);
+    float4 bias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nbase + j * 16 + fq * 4;
+        bias[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, n * 4, 0, 0));
+    }
+    float4 rbuf[2][4];
+    auto load_resid = [&](int i, float4 (&r)[4]) {
+        int m = mbase + i * 16 + fr;
+        if constexpr (CHECK_M) m = m < p.M ? m : p.M - 1;     // clamp: a valid row, result unused
+        const float* rp = p.resid + (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + nbase + fq * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
+    };
+    if constexpr (HAS_RESID) load_resid(0, rbuf[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if constexpr (HAS_RESID) {
+            if (i + 1 < 8) load_resid(i + 1, rbuf[(i + 1) & 1]);
+        }
+        const int m = mbase + i * 16 + fr;
+        if constexpr (CHECK_M) {
+            if (m >= p.M) continue;
+        }
+        const size_t obase = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + nbase + fq * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f32x4 v = acc[i][j];
+            v[0] += bias[j].x; v[1] += bias[j].y; v[2] += bias[j].z; v[3] += bias[j].w;
+            if constexpr (ACT == ACT_GELU) {
+                const f32x2 lo = gelu_pair(f32x2{v[0], v[1]}), hi = gelu_pair(f32x2{v[2], v[3]});
+                v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+            } else {
+                v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
+                v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
+            }
+            if constexpr (HAS_RESID) {
+                const float4 rr = rbuf[i & 1][j];
+                v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+            }
+            if constexpr (OUT_BF16) {
+                uint2 o;
+                o.x = pack_bf2(v[0], v[1]);
+                o.y = pack_bf2(v[2], v[3]);
+                *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + obase + j * 16) = o;
+            } else {
+                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + obase + j * 16) =
+                    make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
+// Epilogue: lane holds C[m = mbase + 16i + (lane&15)][n = nbase + 16j + 4(lane>>4) .. +3].
+// vmcnt counts stores as well as loads and retires in order, so a residual/bias load issued after
+// earlier stores waits for those stores too: bias is loaded once up front and the residual rows of
+// fragment row i+1 are issued before the stores of row i (two-deep register ring).  Column slabs
+// are whole (N % 64 == 0), so the only bounds check is on rows, and only in the last M tile: the
+// interior path has no divergent branch, which keeps hipcc's waitcnt counting exact.
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase, int nbase,
+                                              int lane) {
+    if (nbase >= p.N) return;                                   // wave-uniform
+    if (mbase + 128 <= p.M)
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false>(p, acc, mbase, nbase, lane);
+    else
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true>(p, acc, mbase, nbase, lane);
+}
+
+
 // Bijective XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous range
 // of tile ids so the tiles that share A / W panels run on one L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Tile id -> (tm, tn).  gm <= 1: row-major (all N tiles of one M panel, then the next panel).
+// gm > 1: groups of gm M panels walked column-major, so the ~32 workgroups an XCD runs at once
+// share gm A panels and 32/gm W panels in its L2 instead of 2 A panels and every W panel.
+__device__ __forceinline__ void tile_of(int wgid, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+    if (gm <= 1) {
+        tm = wgid / tiles_n;
+        tn = wgid - tm * tiles_n;
+        return;
+    }
+    const int per = gm * tiles_n;
+    const int g = wgid / per;
+    const int first = g * gm;
+    const int gsz = min(tiles_m - first, gm);
+    const int l = wgid - g * per;
+    tn = l / gsz;
+    tm = first + (l - tn * gsz);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -140,7 +199,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_early(GemmParams p) {
     const int tiles_n = (p.N + BN - 1) / BN;
     const int nwg = ((p.M + BM - 1) / BM) * tiles_n;
     const int wgid = xcd_remap(blockIdx.x, nwg);
-    const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+    int tm, tn;
+    tile_of(wgid, (p.M + BM - 1) / BM, tiles_n, p.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
 
     // staging: thread -> row (tid>>3) + 64*j (j = 0..3), 16-B chunk (tid&7); per wave-instruction
@@ -422,8 +482,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int tm = wgid / tiles_n;
-    const int tn = wgid - tm * tiles_n;
+    int tm, tn;
+    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
 
     const int fr = lane & 15;
@@ -634,8 +694,20 @@ int num_cus() {
     return g_num_cu;
 }
 
+int g_groupm = -1;
+int gemm_groupm() {
+    if (g_groupm < 0) {
+        const char* e = getenv("CE_GEMM_GROUPM");
+        g_groupm = e ? atoi(e) : 4;
+        if (g_groupm < 1 || g_groupm > 64) g_groupm = 1;
+    }
+    return g_groupm;
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
-hipError_t launch_t(const GemmParams& p, hipStream_t s) {
+hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
+    GemmParams p = p0;
+    p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const int sc = gemm_sched();
     if (sc == 9) {
@@ -664,8 +736,10 @@ hipError_t launch_t(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 int set_gemm_schedule(int v) {
-    const int prev = gemm_sched();
-    g_sched = (v == 0 || v == 3 || v == 4 || v == 6 || v == 7 || v == 9) ? v : 1;
+    const int prev = gemm_sched() | (gemm_groupm() << 8);
+    const int sc = v & 0xff, gm = (v >> 8) & 0xff;
+    g_sched = (sc == 0 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9) ? sc : 1;
+    if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }
 

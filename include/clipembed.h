@@ -211,8 +211,9 @@ int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* t
  * act: 0 none, 1 GELU(erf), 2 QuickGELU.  (ResidualAttentionBlock linears, transformer.py:228-239) */
 int ce_kernel_gemm_bf16(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                         int act, const float* resid, void* out, int out_dtype);
-/* Select the GEMM main-loop schedule for subsequent launches (0 = 2-stage whole-tile ring,
- * 1 = 4-phase half-tile ring, the default); returns the previous value.  For A/B measurement. */
+/* Select the GEMM main-loop schedule for subsequent launches (bits 0-7: 0 = 2-stage whole-tile
+ * ring, 1 = 4-phase half-tile ring, the default; bits 8-15: tile-order M-group, 0 = keep);
+ * returns the previous value in the same encoding.  For A/B measurement. */
 int ce_set_gemm_schedule(int schedule);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);

@@ -1,5 +1,6 @@
 """Host-side logic: deterministic generator, config registry, state-dict naming vs the
 reference's key layout (tests/golden/meta.npz), caption format."""
+import os
 import json
 
 import numpy as np
@@ -8,6 +9,8 @@ import pytest
 import clipembed
 from clipembed import weights as W
 from clipembed.config import get_model_config
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_generator_is_pure_and_scaled():
@@ -61,3 +64,26 @@ def test_encoders_refuse_without_device():
     m = clipembed.CLIP(get_model_config("ViT-L-14-336").with_depth(1, 1))
     with pytest.raises(RuntimeError, match="HIP device"):
         m.encode_image(np.zeros((1, 3, 336, 336), np.float32))
+
+
+def test_gelu_polynomial_error_bound():
+    """The GEMM epilogue's packed GELU (csrc/ce_device.h gelu_pair) evaluated in f32 exactly as the
+    device does (clamp, t = 0.08 u^2 - 1, Horner, fma(u, p, 0.5), x * phi): error <= 2.5e-6 * max(1, |y|) vs
+    the exact-erf GELU of nn.GELU (transformer.py:235-239) over all x."""
+    import re
+    from scipy.special import erf
+    src = open(os.path.join(REPO, "clip-embeds_amd", "csrc", "ce_device.h")).read()
+    body = src[src.index("f32x2 gelu_pair"):]
+    body = body[:body.index("return x * phi")]
+    coefs = [np.float32(re.search(r"p = \(f32x2\)\((-?[0-9.e+-]+)f\)", body).group(1))]
+    coefs += [np.float32(c) for c in re.findall(r"fma\(p, t, \(f32x2\)\((-?[0-9.e+-]+)f\)\)", body)]
+    assert len(coefs) == 13
+    x = np.linspace(-12, 12, 200001).astype(np.float32)
+    u = np.clip(x, np.float32(-5), np.float32(5))
+    t = (u * u * np.float32(0.08) - np.float32(1)).astype(np.float32)
+    p = coefs[0]
+    for c in coefs[1:]:
+        p = (p * t + c).astype(np.float32)
+    g = (x * (u * p + np.float32(0.5))).astype(np.float32)
+    ref = 0.5 * x.astype(np.float64) * (1 + erf(x.astype(np.float64) / np.sqrt(2)))
+    assert (np.abs(g - ref) / np.maximum(1.0, np.abs(ref))).max() <= 2.5e-6

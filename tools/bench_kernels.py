@@ -66,8 +66,9 @@ def main():
         O = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
         bufs[name] = (A, W, bias, R, O)
     for rnd in range(args.rounds):
-        for sched in [int(x) for x in args.scheds.split(",")]:
-            _lib.lib().ce_set_gemm_schedule(sched)
+        for sched in args.scheds.split(","):   # "1" or "1g4" (schedule 1, tile-order M-group 4)
+            sc, _, gm = sched.partition("g")
+            _lib.lib().ce_set_gemm_schedule(int(sc) | (int(gm or 1) << 8))
             for name, (M, N, K, act, resid, ob) in shapes.items():
                 A, W, bias, R, O = bufs[name]
 
