@@ -10,7 +10,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libclipembed.so")
+# CLIPEMBED_LIB selects another build of the same library (kernel A/B timing in tools/)
+LIB_PATH = os.environ.get("CLIPEMBED_LIB") or os.path.join(_HERE, "libclipembed.so")
 
 CE_OK, CE_ERR_INVALID, CE_ERR_HIP, CE_ERR_STATE, CE_ERR_OOM = 0, 1, 2, 3, 4
 CE_F32, CE_BF16, CE_F16, CE_I64, CE_I32 = 0, 1, 2, 3, 4

@@ -45,7 +45,7 @@ __device__ __forceinline__ void barrier() {
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int L, int H,
-                                                    float scale_log2) {
+                                                    float qscale) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
@@ -76,6 +76,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+        // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
+        // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
+        if (qscale != 1.0f) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
+        }
     }
 
     // staging: thread -> row tid>>3 of a 32-row pass, 16-B chunk tid&7
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     f32x16 o[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-    float m_run = -INFINITY;
+    float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
     float l_run = 0.f;   // partial (this half's keys)
 
     stage(0, 0);
@@ -140,13 +148,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         // waves whose queries are all padding, or (causal) whose queries all precede this key
         // tile, skip the math but keep the workgroup barriers
         const bool active = q_wave0 < L && !(CAUSAL && t * KBLK > q_wave0 + 31);
+        // second 32-key subtile entirely past the sequence end (L = 577: the last tile holds one
+        // key) or (causal) entirely above this wave's diagonal: skip its MFMAs and exponentials
+        const bool half2 = (t * KBLK + 32 < L) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
         if (active) {
             // ---- S^T = K Q^T (two 32-key subtiles) ----
             f32x16 s[2];
     #pragma unroll
             for (int kt2 = 0; kt2 < 2; ++kt2) {
     #pragma unroll
-                for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+                for (int i = 0; i < 16; ++i) s[kt2][i] = kt2 == 1 && !half2 ? -INFINITY : -m_run;
+                if (kt2 == 1 && !half2) continue;
     #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
@@ -154,7 +166,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 }
             }
 
-            // ---- online softmax (log2 domain, scale folded into one FMA per score) ----
+            // ---- online softmax, log2 domain.  The S accumulator starts at -m_run, so the MFMA
+            // leaves s = q.k - m_run (q pre-scaled): p = exp2(s) needs no per-score FMA ----
             const int key0 = t * KBLK;
             // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
             const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
@@ -173,16 +186,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             for (int kt2 = 0; kt2 < 2; ++kt2)
     #pragma unroll
                 for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax = fmaxf(tmax, s[kt2][i]);
-            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-            const float m_new = fmaxf(m_run, tmax);
-            if (__any(m_new > m_run)) {      // wave-uniform: rescale only when some row max grew
-                const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
-                m_run = m_new;
-                l_run *= alpha;
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));    // relative to m_run
+            // Deferred rescale (guide T13): m_run moves on the first tile (to the exact row max:
+            // key 0 is never masked, so it is finite) and afterwards only when a row max exceeds
+            // it by more than 8, so p <= 2^8 (exact range for the f32 sums and bf16 P) and O / l
+            // are rarely rescaled.  O and l always see the same factor, and the decision precedes
+            // this tile's P, so no P.V product straddles it.
+            if (t == 0 || __any(tmax > 8.0f)) {
+                const float delta = t == 0 ? tmax : fmaxf(tmax, 0.f);
+                if (t != 0) {
+                    const float alpha = __builtin_amdgcn_exp2f(-delta);
+                    l_run *= alpha;
     #pragma unroll
-                for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+                    for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+                }
+                m_run += delta;
+    #pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) s[kt2][i] -= delta;
             }
-            const float mc = m_run * scale_log2;
             float psum = 0.f;
             bf16x8 pf[2][2];
     #pragma unroll
@@ -191,7 +214,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 for (int s2 = 0; s2 < 2; ++s2)
     #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        const float pv = __builtin_amdgcn_exp2f(fmaf(s[kt2][8 * s2 + j], scale_log2, -mc));
+                        if (kt2 == 1 && !half2) { pf[kt2][s2][j] = (__bf16)0.f; continue; }
+                        const float pv = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
                         psum += pv;
                         pf[kt2][s2][j] = (__bf16)pv;
                     }
@@ -202,6 +226,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             for (int kt2 = 0; kt2 < 2; ++kt2)
     #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
+                    if (kt2 == 1 && !half2) continue;
                     const int krow = kt2 * 32 + 16 * s2;
     #pragma unroll
                     for (int dt = 0; dt < 2; ++dt) {
@@ -239,15 +264,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 
 }  // namespace
 
-hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal,
+hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s) {
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
-    const float scale_log2 = 0.125f * 1.4426950408889634f;   // 1/sqrt(64) * log2(e)
+    const float qscale = q_prescaled ? 1.0f : kAttnQScale;
     if (causal)
-        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, scale_log2);
+        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, qscale);
     else
-        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, scale_log2);
+        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, qscale);
     return hipGetLastError();
 }
 

@@ -429,7 +429,7 @@ int run_block(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, int B
         const double flops = 4.0 * B * H * (double)L * L * 64;
         const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
         CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
-                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, causal, s); }));
+                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, causal, true, s); }));
     }
     CE_TRY(gemm(h, s, vis ? "gemm_out_v" : "gemm_out_t", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, w.x,
                 w.x, false));
@@ -653,6 +653,13 @@ int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) 
                 break;
             }
             default: return fail(CE_ERR_INVALID, "ce_load_weights: '%s' unsupported dtype %d", t[i].name, t[i].dtype);
+        }
+        // Fold the attention score scale log2(e)/sqrt(head_dim) into the q rows of in_proj (the
+        // first third of weight and bias): the attention kernel then works in log2 units with no
+        // per-score multiply (attention.hip).  The host-side state dict keeps the original values.
+        if (name.size() > 19 && (name.compare(name.size() - 19, 19, "attn.in_proj_weight") == 0 ||
+                                 name.compare(name.size() - 17, 17, "attn.in_proj_bias") == 0)) {
+            for (size_t j = 0; j < cnt / 3; ++j) f[j] *= ce::kAttnQScale;
         }
         std::vector<char> bytes;
         switch (sp.st) {
@@ -1041,7 +1048,7 @@ int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule);
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal) {
     if (!qkv || !out) return fail(CE_ERR_INVALID, "ce_kernel_attention: null argument");
     if (B <= 0 || L <= 0 || H <= 0) return fail(CE_ERR_INVALID, "ce_kernel_attention: bad sizes");
-    return check_launch(ce::launch_attention((const bf16_t*)qkv, (bf16_t*)out, B, L, H, causal != 0, (hipStream_t)stream),
+    return check_launch(ce::launch_attention((const bf16_t*)qkv, (bf16_t*)out, B, L, H, causal != 0, false, (hipStream_t)stream),
                         "attention");
 }
 

@@ -29,7 +29,10 @@ int set_gemm_schedule(int v);   // returns previous
 // Multi-head attention over a packed QKV activation.
 //   qkv [B*L][3*D] bf16 (q | k | v, head h at columns h*64 .. h*64+63 of each part)
 //   out [B*L][D]   bf16 (heads concatenated), softmax(q k^T / sqrt(64) [+ causal]) v
-hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal,
+// q_prescaled: the q third of qkv already carries kAttnQScale (engine in_proj weights); else the
+// kernel scales its Q fragments.
+constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(64)
+hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s);
 
 // LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.

@@ -226,6 +226,33 @@ def pacl_clip_loss(img, txt, temperature=0.1):
     return (cross_entropy(lpi, lab) + cross_entropy(lpt, lab)) / 2
 
 
+def sparc_masked_pairwise_loss(a, b, mask, scale):
+    """SparcLoss.masked_pairwise_contrastive_loss (pacl.py:527-562): per sample logits
+    scale * a b^T [T,T] + (1 - mask) * -1e8 on the columns, soft-label CE against the identity
+    (= -log_softmax at the diagonal), weighted by mask and normalised by mask.sum()."""
+    logits = (np.einsum("bmd,bnd->bmn", a, b) * F32(scale)).astype(F32)
+    logits = logits + ((F32(1.0) - mask) * F32(-1e8))[:, None, :]
+    m = logits.max(-1, keepdims=True)
+    lse = np.log(np.exp((logits - m).astype(np.float64)).sum(-1)) + m[..., 0]
+    T = a.shape[1]
+    diag = logits[:, np.arange(T), np.arange(T)]
+    loss = lse - diag
+    return float((loss * mask).sum() / mask.sum())
+
+
+def sparc_loss(v_patch, l_tokens, grouped, mask, temperature=0.1):
+    """SparcLoss.forward (pacl.py:564-584): 0.5 * global CLIP loss of the normalised patch /
+    token means + 1.0 * the mean of the two masked local losses."""
+    s = 1.0 / temperature
+    gi = l2normalize(v_patch.mean(1))
+    gt = l2normalize(l_tokens.mean(1))
+    lab = np.arange(gi.shape[0])
+    glob = (cross_entropy(s * gi @ gt.T, lab) + cross_entropy(s * gt @ gi.T, lab)) / 2
+    local = (sparc_masked_pairwise_loss(grouped, l_tokens, mask, s) +
+             sparc_masked_pairwise_loss(l_tokens, grouped, mask, s)) / 2
+    return 0.5 * glob + 1.0 * local
+
+
 def negclip_local_loss(imgs, txts, per_rank_B, rank, scale):
     """open_clip ClipLoss(local_loss=True, usehardtext=True) on rank `rank` (loss.py:137-193):
     imgs[r] [B,D], txts[r] [B+K_r, D] for every rank r."""

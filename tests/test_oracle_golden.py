@@ -104,6 +104,9 @@ def test_sparc(golden):
         assert rel(lnorm, g[f"{name}_l_norm"]) < 1e-6
         gl = O.l2normalize(grouped.mean(1)) @ O.l2normalize(lnorm.mean(1)).T
         np.testing.assert_allclose(gl, g[f"{name}_score_local"], rtol=1e-5, atol=1e-6)
+        mask = (np.arange(77)[None, :] <= np.array([[20], [76]])).astype(np.float32)
+        loss = O.sparc_loss(v, g[f"{name}_l_norm"], g[f"{name}_grouped"], mask, 0.1)
+        np.testing.assert_allclose(loss, g[f"{name}_sparc_loss"], rtol=1e-5)
 
 
 def test_losses(golden):

@@ -6,6 +6,7 @@ interleaved A/B of GEMM schedules in one process (guide §5.4 rule 24).
 import argparse
 import ctypes
 import json
+import time
 import os
 import sys
 
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--scheds", default="0,1")
+    ap.add_argument("--warm-s", type=float, default=2.0)
     ap.add_argument("--only", default="", help="comma list of shape names to run (default all)")
     args = ap.parse_args()
     B = args.batch
@@ -55,6 +57,14 @@ def main():
         keep = set(args.only.split(","))
         shapes = {k: v for k, v in shapes.items() if k in keep}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    # bring the clocks up before the first timed shape (~2 s of dense bf16 matmul)
+    xw = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    t0 = time.time()
+    while time.time() - t0 < args.warm_s:
+        for _ in range(20):
+            xw @ xw
+        torch.cuda.synchronize()
+    del xw
     g = torch.Generator(device="cuda").manual_seed(0)
     res = {}
     bufs = {}
