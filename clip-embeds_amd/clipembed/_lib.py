@@ -78,6 +78,8 @@ _SIGNATURES = {
                                 c_void_p, c_void_p]),
     "ce_sparc_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                  c_void_p, c_void_p, c_void_p]),
+    "ce_sparc_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                              c_int, c_float, c_float, c_float, c_void_p]),
     "ce_apply_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "ce_set_kernel_timing": (c_int, [c_void_p, c_int]),
     "ce_kernel_stats": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_double), POINTER(c_int64),

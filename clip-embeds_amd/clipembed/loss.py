@@ -72,8 +72,14 @@ class ClipLoss:
         self.usehardtext = usehardtext
         self.engine = engine
 
+    def _engine(self, t: torch.Tensor):
+        if self.engine is None:
+            from .model import kernel_engine
+            self.engine = kernel_engine(t.device)
+        return self.engine
+
     def _logits(self, a: torch.Tensor, b: torch.Tensor, scale: float) -> torch.Tensor:
-        e = self.engine
+        e = self._engine(a)
         a = a.float().contiguous()
         b = b.float().contiguous()
         out = torch.empty(a.shape[0], b.shape[0], device=a.device, dtype=torch.float32)
@@ -82,7 +88,7 @@ class ClipLoss:
         return out
 
     def _ce(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        e = self.engine
+        e = self._engine(logits)
         out = torch.empty((), device=logits.device, dtype=torch.float32)
         labels = labels.to(torch.int64).contiguous()
         _lib.call("ce_cross_entropy", e.h, _stream(e.device), _ptr(logits), logits.shape[0], logits.shape[1],

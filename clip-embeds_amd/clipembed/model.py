@@ -119,6 +119,22 @@ class Engine:
         return out
 
 
+
+_KERNEL_ENGINES: Dict[int, "Engine"] = {}
+
+
+def kernel_engine(device) -> "Engine":
+    """A weightless handle per device for the loss / head entry points that need no tower weights
+    (ce_get_logits, ce_cross_entropy, ce_sparc_loss ...): lets the reference's loss classes keep
+    their constructor signatures (pacl.py:489-521, open_clip loss.py:89-103)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError(f"clipembed runs on the GPU only (got a tensor on {device})")
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _KERNEL_ENGINES:
+        _KERNEL_ENGINES[idx] = Engine(get_model_config("ViT-L-14-336"), idx)
+    return _KERNEL_ENGINES[idx]
+
 class VisualTower:
     """Stands in for `model.visual` (attributes read or toggled by the reference callers)."""
 

@@ -6,6 +6,7 @@ Class names and forward signatures follow the reference so eval drivers read the
   open_clip_pacl_rope_after pacl.py:199-209 (RoPE on projected tokens, sigmoid(10 cos) weights)
   sparc                     pacl.py:380-478 (forward / scoring / forward_text mask)
   apply_rope                pacl.py:147-181
+  ClipLoss, SparcLoss       pacl.py:486-584 (temperature-scaled CLIP loss; SPARC global + masked local)
 Everything runs through libclipembed; the fused pooling is ce_pacl_pool.
 """
 from __future__ import annotations
@@ -14,7 +15,7 @@ import torch
 
 from . import _lib
 from .config import get_model_config
-from .model import CLIP, _ptr, _stream
+from .model import CLIP, _ptr, _stream, kernel_engine
 from .weights import synthetic_pacl_heads
 
 
@@ -193,3 +194,70 @@ class sparc(open_clip_pacl):
         else:
             gi = torch.nn.functional.normalize(g.mean(dim=1), dim=-1)
         return self.clip_model.logits(gi, gt, 1.0, with_text_logits=False)[0]
+
+
+class ClipLoss(torch.nn.Module):
+    """PACL ClipLoss (pacl.py:486-514): logit_scale = 1 / temperature, labels arange, mean of the
+    image->text and text->image cross entropies.  Logits and CE run in libclipembed."""
+
+    def __init__(self, temperature: float, engine=None):
+        super().__init__()
+        self.logit_scale = 1.0 / temperature
+        self.engine = engine
+
+    def _engine(self, t: torch.Tensor):
+        return self.engine if self.engine is not None else kernel_engine(t.device)
+
+    def get_ground_truth(self, device, num_logits: int) -> torch.Tensor:
+        return torch.arange(num_logits, device=device, dtype=torch.long)
+
+    @torch.no_grad()
+    def get_logits(self, image_features, text_features):
+        e = self._engine(image_features)
+        a = image_features.float().contiguous()
+        b = text_features.float().contiguous()
+        lpi = torch.empty(a.shape[0], b.shape[0], device=a.device, dtype=torch.float32)
+        lpt = torch.empty(b.shape[0], a.shape[0], device=a.device, dtype=torch.float32)
+        _lib.call("ce_get_logits", e.h, _stream(e.device), _ptr(a), a.shape[0], _ptr(b), b.shape[0], a.shape[1],
+                  float(self.logit_scale), 0, _ptr(lpi), _ptr(lpt))
+        return lpi, lpt
+
+    def _ce(self, e, logits, labels):
+        out = torch.empty((), device=logits.device, dtype=torch.float32)
+        _lib.call("ce_cross_entropy", e.h, _stream(e.device), _ptr(logits), logits.shape[0], logits.shape[1],
+                  _ptr(labels), _ptr(out))
+        return out
+
+    @torch.no_grad()
+    def forward(self, image_features, text_features):
+        e = self._engine(image_features)
+        lpi, lpt = self.get_logits(image_features, text_features)
+        labels = self.get_ground_truth(image_features.device, lpi.shape[0])
+        return (self._ce(e, lpi, labels) + self._ce(e, lpt, labels)) / 2
+
+
+class SparcLoss(ClipLoss):
+    """SparcLoss (pacl.py:516-584): global_weight * CLIP loss of the normalised patch / token means
+    + local_weight * the mean of the two masked pairwise local losses — one ce_sparc_loss call."""
+
+    def __init__(self, temperature: float, engine=None):
+        super().__init__(temperature, engine)
+        self.global_weight = 0.5
+        self.local_weight = 1.0
+
+    @torch.no_grad()
+    def forward(self, v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask):
+        e = self._engine(v_patch_embed)
+        v = v_patch_embed.float().contiguous()
+        lt = l_token_embed.float().contiguous()
+        g = l_grouped_v_patch_embed.float().contiguous()
+        m = language_mask.float().contiguous()
+        B, P, D = v.shape
+        T = lt.shape[1]
+        if lt.shape != (B, T, D) or g.shape != (B, T, D) or m.shape != (B, T):
+            raise ValueError(f"SparcLoss: shape mismatch v {tuple(v.shape)} l {tuple(lt.shape)} "
+                             f"g {tuple(g.shape)} mask {tuple(m.shape)}")
+        out = torch.empty((), device=v.device, dtype=torch.float32)
+        _lib.call("ce_sparc_loss", e.h, _stream(e.device), _ptr(v), _ptr(lt), _ptr(g), _ptr(m), B, P, T, D,
+                  1.0 / float(self.logit_scale), float(self.global_weight), float(self.local_weight), _ptr(out))
+        return out

@@ -988,6 +988,50 @@ int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l,
     return CE_OK;
 }
 
+int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float* l_tokens, const float* grouped,
+                  const float* mask, int B, int P, int T, int D, float temperature, float global_weight,
+                  float local_weight, float* out_loss) {
+    if (!h || !v_patch || !l_tokens || !grouped || !mask || !out_loss)
+        return fail(CE_ERR_INVALID, "ce_sparc_loss: null argument");
+    if (B <= 0 || P <= 0 || T <= 0 || D <= 0 || !(temperature > 0.f))
+        return fail(CE_ERR_INVALID, "ce_sparc_loss: bad sizes or temperature");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const float scale = 1.0f / temperature;   // ClipLoss.logit_scale (pacl.py:491-493)
+    const size_t nGI = (size_t)B * D, nG = (size_t)B * B, nS = (size_t)B * T * T;
+    CE_TRY(ensure_tmp(h, (2 * nGI + 2 * nG + nS + 5 * (size_t)B) * 4));
+    float* gi = (float*)h->tmp;
+    float* gt = gi + nGI;
+    float* G = gt + nGI;
+    float* Gt = G + nG;
+    float* S = Gt + nG;
+    float* lr = S + nS;
+    float* lc = lr + B;
+    float* part = lc + B;
+    // global: normalise the patch / token means, CLIP loss both ways (pacl.py:566-576)
+    CE_TRY(check_launch(ce::launch_mean_mid(gi, v_patch, B, P, D, s), "sparc_loss mean"));
+    CE_TRY(check_launch(ce::launch_mean_mid(gt, l_tokens, B, T, D, s), "sparc_loss mean"));
+    CE_TRY(check_launch(ce::launch_l2norm(gi, gi, B, D, s), "sparc_loss normalize"));
+    CE_TRY(check_launch(ce::launch_l2norm(gt, gt, B, D, s), "sparc_loss normalize"));
+    ce::FGemmParams a{};
+    a.A = gi; a.lda = D; a.B = gt; a.ldb = D; a.C = G; a.ldc = B;
+    a.M = B; a.N = B; a.K = D; a.batch = 1; a.alpha = scale; a.Ct = Gt; a.ldct = B;
+    CE_TRY(check_launch(ce::launch_fgemm(a, true, s), "sparc_loss global logits"));
+    CE_TRY(check_launch(ce::launch_ce_diag_rows(lr, G, B, B, s), "sparc_loss ce"));
+    CE_TRY(check_launch(ce::launch_ce_diag_rows(lc, Gt, B, B, s), "sparc_loss ce"));
+    // local: S[b] = scale * grouped[b] l[b]^T, masked CE over rows and columns (pacl.py:578-582)
+    ce::FGemmParams c{};
+    c.A = grouped; c.lda = D; c.sA = (long)T * D;
+    c.B = l_tokens; c.ldb = D; c.sB = (long)T * D;
+    c.C = S; c.ldc = T; c.sC = (long)T * T;
+    c.M = T; c.N = T; c.K = D; c.batch = B; c.alpha = scale;
+    CE_TRY(timed(h, s, "sparc_loss_local", 2.0 * B * T * T * D, 4.0 * B * (2.0 * T * D + (double)T * T),
+                 [&] { return ce::launch_fgemm(c, true, s); }));
+    CE_TRY(check_launch(ce::launch_sparc_local(part, S, mask, B, T, s), "sparc_loss local"));
+    return check_launch(ce::launch_sparc_loss_finish(out_loss, lr, lc, part, B, global_weight, local_weight, s),
+                        "sparc_loss finish");
+}
+
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out) {
     if (!h || !x || !out) return fail(CE_ERR_INVALID, "ce_apply_rope: null argument");
     if (B <= 0 || P <= 0 || D <= 0 || D % 2) return fail(CE_ERR_INVALID, "ce_apply_rope: bad sizes");

@@ -93,4 +93,11 @@ hipError_t launch_rope(float* out, const float* x, int B, int P, int D, const fl
                        const float* sin_t, hipStream_t s);
 hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t s);
 
+// SparcLoss pieces (pacl.py:516-584)
+hipError_t launch_mean_mid(float* out, const float* x, int B, int P, int D, hipStream_t s);   // mean over dim 1
+hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, hipStream_t s);     // per-row CE vs arange
+hipError_t launch_sparc_local(float* part, const float* S, const float* mask, int B, int T, hipStream_t s);
+hipError_t launch_sparc_loss_finish(float* out, const float* lr, const float* lc, const float* part, int B,
+                                    float global_weight, float local_weight, hipStream_t s);
+
 }  // namespace ce

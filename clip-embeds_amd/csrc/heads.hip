@@ -241,4 +241,125 @@ hipError_t launch_sparc_weights(float* sim, long rows, int P, float sigma, hipSt
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// SparcLoss (pacl.py:516-584)
+
+namespace {
+
+// out[b][d] = mean_p x[b][p][d]   (torch.mean(dim=1), pacl.py:566-567)
+__global__ __launch_bounds__(256) void mean_mid_k(const float* __restrict__ x, float* __restrict__ out, int P,
+                                                  int D) {
+    const int b = blockIdx.y;
+    const int d = blockIdx.x * 256 + threadIdx.x;
+    if (d >= D) return;
+    const float* xp = x + (size_t)b * P * D + d;
+    float acc = 0.f;
+    for (int p = 0; p < P; ++p) acc += xp[(size_t)p * D];
+    out[(size_t)b * D + d] = acc / (float)P;
+}
+
+// loss[i] = logsumexp_j L[i][j] - L[i][i]  (F.cross_entropy against arange labels, per row); wave per row
+__global__ __launch_bounds__(256) void ce_diag_rows_k(const float* __restrict__ L, int R, int C,
+                                                      float* __restrict__ loss) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= R) return;
+    const float* lr = L + (size_t)row * C;
+    float m = -INFINITY;
+    for (int j = lane; j < C; j += 64) m = fmaxf(m, lr[j]);
+    m = wave_max(m);
+    float sum = 0.f;
+    for (int j = lane; j < C; j += 64) sum += __expf(lr[j] - m);
+    sum = wave_sum(sum);
+    if (lane == 0) loss[row] = logf(sum) + m - lr[row];
+}
+
+// Masked pairwise local loss, both directions, for one sample per block (pacl.py:527-562):
+// S = scale * grouped l^T [T][T]; vl row i: logits S[i][j] + (1 - mask[j]) * -1e8; lv row i (the
+// transposed product) = column i of S with the same column mask.  part[b] = {sum_i mask_i
+// (lse_vl_i - S_ii), sum_i mask_i (lse_lv_i - S_ii), sum_i mask_i}.
+__global__ __launch_bounds__(256) void sparc_local_k(const float* __restrict__ S, const float* __restrict__ mask,
+                                                     int T, float* __restrict__ part) {
+    const int b = blockIdx.x;
+    const float* Sb = S + (size_t)b * T * T;
+    const float* mb = mask + (size_t)b * T;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int i = threadIdx.x; i < T; i += blockDim.x) {
+        float mr = -INFINITY, mc = -INFINITY;
+        for (int j = 0; j < T; ++j) {
+            const float pen = (1.0f - mb[j]) * -1e8f;
+            mr = fmaxf(mr, Sb[(size_t)i * T + j] + pen);
+            mc = fmaxf(mc, Sb[(size_t)j * T + i] + pen);
+        }
+        float sr = 0.f, sc = 0.f;
+        for (int j = 0; j < T; ++j) {
+            const float pen = (1.0f - mb[j]) * -1e8f;
+            sr += __expf(Sb[(size_t)i * T + j] + pen - mr);
+            sc += __expf(Sb[(size_t)j * T + i] + pen - mc);
+        }
+        const float dg = Sb[(size_t)i * T + i] + (1.0f - mb[i]) * -1e8f;
+        const float w = mb[i];
+        a0 += w * (logf(sr) + mr - dg);
+        a1 += w * (logf(sc) + mc - dg);
+        a2 += w;
+    }
+    __shared__ float red[3][4];
+    a0 = wave_sum(a0); a1 = wave_sum(a1); a2 = wave_sum(a2);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][wv] = a0; red[1][wv] = a1; red[2][wv] = a2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        float t = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[threadIdx.x][w];
+        part[(size_t)b * 3 + threadIdx.x] = t;
+    }
+}
+
+// total = wg * (mean(lr) + mean(lc)) / 2 + wl * (P0 / M + P1 / M) / 2; fixed summation order
+__global__ __launch_bounds__(256) void sparc_loss_finish_k(const float* __restrict__ lr, const float* __restrict__ lc,
+                                                           const float* __restrict__ part, int B, float wg, float wl,
+                                                           float* __restrict__ out) {
+    float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < B; i += 256) {
+        v[0] += lr[i]; v[1] += lc[i];
+        v[2] += part[3 * i]; v[3] += part[3 * i + 1]; v[4] += part[3 * i + 2];
+    }
+    __shared__ float red[5][4];
+    const int wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const float t = wave_sum(v[k]);
+        if ((threadIdx.x & 63) == 0) red[k][wv] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t[5];
+        for (int k = 0; k < 5; ++k) t[k] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
+        const float glob = (t[0] / (float)B + t[1] / (float)B) * 0.5f;
+        const float local = (t[2] / t[4] + t[3] / t[4]) * 0.5f;
+        out[0] = wg * glob + wl * local;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_mean_mid(float* out, const float* x, int B, int P, int D, hipStream_t s) {
+    hipLaunchKernelGGL(mean_mid_k, dim3((unsigned)((D + 255) / 256), (unsigned)B), dim3(256), 0, s, x, out, P, D);
+    return hipGetLastError();
+}
+hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, hipStream_t s) {
+    hipLaunchKernelGGL(ce_diag_rows_k, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, L, R, C, loss);
+    return hipGetLastError();
+}
+hipError_t launch_sparc_local(float* part, const float* S, const float* mask, int B, int T, hipStream_t s) {
+    hipLaunchKernelGGL(sparc_local_k, dim3((unsigned)B), dim3(128), 0, s, S, mask, T, part);
+    return hipGetLastError();
+}
+hipError_t launch_sparc_loss_finish(float* out, const float* lr, const float* lc, const float* part, int B,
+                                    float global_weight, float local_weight, hipStream_t s) {
+    hipLaunchKernelGGL(sparc_loss_finish_k, dim3(1), dim3(256), 0, s, lr, lc, part, B, global_weight, local_weight,
+                       out);
+    return hipGetLastError();
+}
+
 }  // namespace ce

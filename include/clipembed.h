@@ -194,6 +194,17 @@ int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l,
                      int T, int D, float sigma, float* out_grouped, float* out_l_norm,
                      float* out_sim);
 
+/* SparcLoss.forward (Patch-Aligned-Contrastive-Learning/model/pacl.py:564-584, masked local loss
+ * :527-562): global_weight (reference 0.5, :520) * CLIP loss (logit scale 1/temperature) of the
+ * L2-normalised means of v_patch over P and of l_tokens over T, + local_weight (reference 1.0,
+ * :521) * the mean of the two masked pairwise local losses between
+ * grouped and l_tokens.  v_patch f32 [B,P,D] (projected patches, unnormalised), l_tokens f32 [B,T,D]
+ * and grouped f32 [B,T,D] (both L2-normalised, as ce_sparc_forward returns them), mask f32 [B,T]
+ * (1 = token <= EOT).  out_loss: device f32 [1]. */
+int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float* l_tokens, const float* grouped,
+                  const float* mask, int B, int P, int T, int D, float temperature, float global_weight,
+                  float local_weight, float* out_loss);
+
 /* apply_rope (pacl.py:147-181): de-interleaving rotary embedding over positions 0..P-1.
  * x, out: device f32 [B,P,D] (may alias). */
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out);

@@ -222,6 +222,50 @@ def test_sparc_vs_golden(pacl_models, golden, name, sigma):
                                atol=1e-4)
 
 
+@pytest.mark.parametrize("name,sigma", [("s576", 1.0 / 576), ("s625", 1.0 / 625)])
+def test_sparc_loss_vs_golden(golden, name, sigma):
+    """SparcLoss (pacl.py:516-584) through ce_sparc_loss on the reference's own (v, l_norm,
+    grouped) fixture, mask = tokens <= EOT at 20 and 76; rtol 1e-5 (f32 sums of 2x77 rows)."""
+    from clipembed.pacl import SparcLoss
+    g = golden("sparc")
+    v = torch.from_numpy(W.uniform("sparc-v", 2 * 576 * 64).reshape(2, 576, 64)).cuda()
+    lt = torch.from_numpy(g[f"{name}_l_norm"]).cuda()
+    gr = torch.from_numpy(g[f"{name}_grouped"]).cuda()
+    mask = torch.from_numpy((np.arange(77)[None, :] <= np.array([[20], [76]])).astype(np.float32)).cuda()
+    loss = SparcLoss(0.1)(v, lt, gr, mask)
+    np.testing.assert_allclose(float(loss), float(g[f"{name}_sparc_loss"]), rtol=1e-5)
+
+
+def test_sparc_loss_vs_oracle_ragged():
+    """Larger batch with ragged masks (one sample with only SOT+EOT valid) and non-default
+    weights/temperature vs the oracle restatement."""
+    from clipembed.pacl import SparcLoss
+    B, P, T, D = 6, 576, 77, 96
+    v = W.uniform("sl-v", B * P * D).reshape(B, P, D)
+    lt = O.l2normalize(W.uniform("sl-l", B * T * D).reshape(B, T, D))
+    gr = O.l2normalize(W.uniform("sl-g", B * T * D).reshape(B, T, D))
+    eot = np.array([1, 5, 20, 40, 76, 33])
+    mask = (np.arange(T)[None, :] <= eot[:, None]).astype(np.float32)
+    fn = SparcLoss(0.07)
+    fn.global_weight, fn.local_weight = 0.3, 0.7
+    got = float(fn(*(torch.from_numpy(x).cuda() for x in (v, lt, gr, mask))))
+    s = 1.0 / 0.07
+    gi, gt = O.l2normalize(v.mean(1)), O.l2normalize(lt.mean(1))
+    lab = np.arange(B)
+    glob = (O.cross_entropy(s * gi @ gt.T, lab) + O.cross_entropy(s * gt @ gi.T, lab)) / 2
+    local = (O.sparc_masked_pairwise_loss(gr, lt, mask, s) + O.sparc_masked_pairwise_loss(lt, gr, mask, s)) / 2
+    np.testing.assert_allclose(got, 0.3 * glob + 0.7 * local, rtol=2e-5)
+
+
+def test_pacl_clip_loss_mirror(golden):
+    """pacl.py ClipLoss(temperature) mirror on a weightless kernel handle."""
+    from clipembed.pacl import ClipLoss as PaclClipLoss
+    g = golden("loss")
+    a = torch.from_numpy(O.l2normalize(W.uniform("loss-a", 8 * 768).reshape(8, 768))).cuda()
+    b = torch.from_numpy(O.l2normalize(W.uniform("loss-b", 8 * 768).reshape(8, 768))).cuda()
+    np.testing.assert_allclose(float(PaclClipLoss(0.1)(a, b)), float(g["pacl_clip_loss"]), rtol=1e-5)
+
+
 def test_logits_and_cross_entropy(small, golden):
     from clipembed.loss import ClipLoss
     g = golden("loss")
