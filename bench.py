@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="image-text pairs per GPU per step")
-    ap.add_argument("--cpu-pairs", type=int, default=2, help="pairs in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-pairs", type=int, default=8, help="pairs in the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     args = ap.parse_args()

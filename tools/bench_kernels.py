@@ -78,7 +78,7 @@ def main():
     for rnd in range(args.rounds):
         for sched in args.scheds.split(","):   # "1" or "1g4" (schedule 1, tile-order M-group 4)
             sc, _, gm = sched.partition("g")
-            _lib.lib().ce_set_gemm_schedule(int(sc) | (int(gm or 1) << 8))
+            _lib.lib().ce_set_gemm_schedule(int(sc) | (int(gm or 0) << 8))   # g0 = keep the default
             for name, (M, N, K, act, resid, ob) in shapes.items():
                 A, W, bias, R, O = bufs[name]
 

@@ -6,11 +6,12 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 SHAPES=${1:-qkv_v,fc_v,out_v,proj_v,attn_v,ln_v}
-mkdir -p gpurun_out/pmct
+OUT=${2:-gpurun_out/pmct}   # e.g. run with CE_GEMM_GROUPM=8 into another directory
+mkdir -p $OUT
 for s in ${SHAPES//,/ }; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    d=gpurun_out/pmct/${s}_${c}
+    d=$OUT/${s}_${c}
     timeout -k 10 180 rocprofv3 --kernel-trace --pmc $c -d $d -o run --output-format csv -- \
-      python3 tools/bench_kernels.py --rounds 1 --reps 3 --scheds 1 --only $s > $d.log 2>&1
+      python3 tools/bench_kernels.py --rounds 1 --reps 3 --warm-s 0 --scheds 1 --only $s > $d.log 2>&1
   done
 done
