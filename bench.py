@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--cpu-pairs", type=int, default=8, help="pairs in the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    ap.add_argument("--text-stream", action="store_true", help="run the text tower on a second stream")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,9 +110,22 @@ def main():
     scale = float(model.logit_scale.detach().exp())
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s, batch {B}/GPU, world {world}")
 
+    side = torch.cuda.Stream(dev)
+    main_stream = torch.cuda.current_stream(dev)
+
     def step():
-        fi = model.encode_image(imgs, normalize=True)
-        ft = model.encode_text(caps, normalize=True)
+        if args.text_stream:
+            # the text tower (its own workspace in the engine) on a second stream, overlapping the
+            # vision tower's tile tails and row kernels
+            side.wait_stream(main_stream)
+            with torch.cuda.stream(side):
+                ft = model.encode_text(caps, normalize=True)
+            fi = model.encode_image(imgs, normalize=True)
+            main_stream.wait_stream(side)
+            ft.record_stream(main_stream)
+        else:
+            fi = model.encode_image(imgs, normalize=True)
+            ft = model.encode_text(caps, normalize=True)
         if world > 1:
             ai = all_gather_cat(fi, world)          # RCCL all-gather over xGMI
             at = all_gather_cat(ft, world)

@@ -132,8 +132,10 @@ struct ce_handle {
     int Kp = 0;      // padded patch K
     int G = 0;       // patch grid side
     // workspace
-    char* ws = nullptr;
+    char* ws = nullptr;      // vision tower (and PACL / sequential paths)
     size_t ws_bytes = 0;
+    char* ws_t = nullptr;    // text tower: its own buffers, so encode_text may run on another stream
+    size_t ws_t_bytes = 0;   // concurrently with encode_image
     char* tmp = nullptr;
     size_t tmp_bytes = 0;
     float* scratch = nullptr;    // 256 B
@@ -354,20 +356,22 @@ size_t text_bytes(const ce_handle* h, long B) {
     return tower_bytes(B * h->cfg.context_length, h->cfg.text.width, h->cfg.text.mlp_width, 0, B);
 }
 
-int ensure_ws(ce_handle* h, size_t need) {
-    if (need <= h->ws_bytes) return CE_OK;
+int grow_buffer(char*& buf, size_t& bytes, size_t need) {
+    if (need <= bytes) return CE_OK;
     HIP_TRY(hipDeviceSynchronize());
-    if (h->ws) HIP_TRY(hipFree(h->ws));
-    h->ws = nullptr;
-    h->ws_bytes = 0;
-    if (hipMalloc(&h->ws, need) != hipSuccess) {
-        h->ws = nullptr;
+    if (buf) HIP_TRY(hipFree(buf));
+    buf = nullptr;
+    bytes = 0;
+    if (hipMalloc(&buf, need) != hipSuccess) {
+        buf = nullptr;
         (void)hipGetLastError();
         return fail(CE_ERR_OOM, "cannot allocate %zu bytes of workspace", need);
     }
-    h->ws_bytes = need;
+    bytes = need;
     return CE_OK;
 }
+int ensure_ws(ce_handle* h, size_t need) { return grow_buffer(h->ws, h->ws_bytes, need); }
+int ensure_ws_text(ce_handle* h, size_t need) { return grow_buffer(h->ws_t, h->ws_t_bytes, need); }
 
 int ensure_tmp(ce_handle* h, size_t need) {
     if (need <= h->tmp_bytes) return CE_OK;
@@ -598,6 +602,7 @@ int ce_destroy(ce_handle* h) {
     (void)hipDeviceSynchronize();
     for (auto& kv : h->dptr) (void)hipFree(kv.second);
     if (h->ws) (void)hipFree(h->ws);
+    if (h->ws_t) (void)hipFree(h->ws_t);
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->scratch) (void)hipFree(h->scratch);
     for (float* p : {h->rc_v, h->rs_v, h->rc_p, h->rs_p})
@@ -726,7 +731,8 @@ int ce_missing_weights(ce_handle* h, int* n_missing, const char** first_missing)
 int ce_reserve(ce_handle* h, int max_images, int max_texts) {
     if (!h || max_images < 0 || max_texts < 0) return fail(CE_ERR_INVALID, "ce_reserve: bad argument");
     DeviceGuard g(h->device);
-    return ensure_ws(h, std::max(vision_bytes(h, max_images), text_bytes(h, max_texts)));
+    CE_TRY(ensure_ws(h, std::max(vision_bytes(h, max_images), text_bytes(h, max_texts))));
+    return ensure_ws_text(h, text_bytes(h, max_texts));
 }
 
 int ce_encode_image(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int B, int normalize,
@@ -764,9 +770,9 @@ int ce_encode_text(ce_handle* h, void* stream, const int64_t* ids, int B, int ct
     CE_TRY(check_ready(h, false));
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
-    CE_TRY(ensure_ws(h, text_bytes(h, B)));
+    CE_TRY(ensure_ws_text(h, text_bytes(h, B)));
     const int D = h->cfg.text.width;
-    TowerWs w = carve(h->ws, (long)B * ctx, D, h->cfg.text.mlp_width, 0, B);
+    TowerWs w = carve(h->ws_t, (long)B * ctx, D, h->cfg.text.mlp_width, 0, B);
     CE_TRY(run_text(h, s, w, ids, B, out_pooled, normalize != 0));
     if (out_tokens)
         CE_TRY(layernorm(h, s, "ln_t", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "ln_final.weight"),

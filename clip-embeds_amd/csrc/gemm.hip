@@ -80,25 +80,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int
                                              0x00020000);
 }
 
-template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M>
-__device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase,
+template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ>
+__device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase,
                                                    int nbase, int lane) {
     const int fr = lane & 15, fq = lane >> 4;
     // bias through a buffer descriptor: a null bias gets num_records 0 and reads zeros, with no branch
     const __amdgpu_buffer_rsrc_t bsrd = make_srd(p.bias ? (const void*)p.bias : (const void*)p.A, p.bias ? p.N * 4 : 0);
-    float4 bias[4];
+    float4 bias[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
         const int n = nbase + j * 16 + fq * 4;
         bias[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(bsrd, n * 4, 0, 0));
     }
-    float4 rbuf[2][4];
-    auto load_resid = [&](int i, float4 (&r)[4]) {
+    // 16-column blocks inside N (wave-uniform; N % 64 == 0, so a 64-column slab is whole and only
+    // the 128-column slabs of SCHED 2 can be cut)
+    const int jmax = NJ > 4 ? min(NJ, (p.N - nbase) / 16) : NJ;
+    float4 rbuf[2][NJ];
+    auto load_resid = [&](int i, float4 (&r)[NJ]) {
         int m = mbase + i * 16 + fr;
         if constexpr (CHECK_M) m = m < p.M ? m : p.M - 1;     // clamp: a valid row, result unused
         const float* rp = p.resid + (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + nbase + fq * 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
+        for (int j = 0; j < NJ; ++j)
+            if (j < jmax) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
     };
     if constexpr (HAS_RESID) load_resid(0, rbuf[0]);
 #pragma unroll
@@ -112,7 +116,8 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         }
         const size_t obase = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + nbase + fq * 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
+            if (j >= jmax) break;
             f32x4 v = acc[i][j];
             v[0] += bias[j].x; v[1] += bias[j].y; v[2] += bias[j].z; v[3] += bias[j].w;
             if constexpr (ACT == ACT_GELU) {
@@ -145,14 +150,14 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
 // fragment row i+1 are issued before the stores of row i (two-deep register ring).  Column slabs
 // are whole (N % 64 == 0), so the only bounds check is on rows, and only in the last M tile: the
 // interior path has no divergent branch, which keeps hipcc's waitcnt counting exact.
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][4], int mbase, int nbase,
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int NJ = 4>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase, int nbase,
                                               int lane) {
     if (nbase >= p.N) return;                                   // wave-uniform
     if (mbase + 128 <= p.M)
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false, NJ>(p, acc, mbase, nbase, lane);
     else
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true, NJ>(p, acc, mbase, nbase, lane);
 }
 
 
@@ -669,13 +674,127 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
 }
 
+// ------------------------------------------------------------------------------------------
+// SCHED 2 ("w4"): the 256x256 tile computed by FOUR waves (one per SIMD), each owning a 128x128
+// quadrant: acc[8][8] = 256 f32 per lane pinned in AGPRs, so a fragment read feeds 8 MFMAs (LDS
+// reads per MFMA 0.25 vs 0.44 for SCHED 1).  One wave per SIMD has no partner to hide latency, so
+// the pipeline is explicit: BK = 32 steps through a 4-slot LDS ring (32 KB per slot: A and W
+// 256 rows x 64 B, chunk c of row r at c ^ ((r>>2)&3), conflict-free ds_read_b128), DMA issued
+// four steps ahead (slots 0..3 in flight from the prologue), fragments of step s+1 read while
+// the 64 MFMAs of step s run:
+//    [frags(s) in regs] wait DMA(s+1) | barrier | DMA(s+4) -> slot s%4 | read frags(s+1) | MFMA(s)
+// One barrier per step.
+constexpr int W4_BK = 32;
+constexpr int W4_SLOT = 2 * BM * W4_BK * 2;     // 32 KB: A then W
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_w4(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * W4_SLOT];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int wgid = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // staging: wave-instruction j moves rows j*64 + wave*16 + (lane>>2), 64-B row segments
+    const int srow = wave * 16 + (lane >> 2);
+    const int schunk = (lane & 3) ^ ((srow >> 2) & 3);       // (j*64 + srow) >> 2 & 3 == srow >> 2 & 3
+    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
+    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
+    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
+    const __amdgpu_buffer_rsrc_t srdW = make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, BN)) * (int)p.ldw * 2);
+    const int lds_wave = wave * 1024;
+    const int ns = p.K / W4_BK;      // even, >= 2 (K % 64 == 0)
+    // steps past K are still issued (the loop stays branch-free and vmcnt counts stay constant)
+    // but with an offset beyond the descriptor's range: no memory traffic, LDS slot never read
+    auto stage = [&](int ks) {
+        char* base = smem + (ks & 3) * W4_SLOT + lds_wave;
+        const int kb = ks < ns ? ks * W4_BK * 2 : 0x7ffff000;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + j * 4096), 16,
+                                                     voffA + j * 64 * (int)p.lda * 2, kb, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + W4_SLOT / 2 + j * 4096), 16,
+                                                     voffW + j * 64 * (int)p.ldw * 2, kb, 0, 0);
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int frag_off = fr * 64 + ((fq ^ ((fr >> 2) & 3)) << 4);
+    const int a_off = wm * 128 * 64 + frag_off;
+    const int w_off = W4_SLOT / 2 + wn * 128 * 64 + frag_off;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 af[2][8], bf[2][8];   // [register set][block]
+    auto read_b = [&](int ks, int r) {
+        const char* sb = smem + (ks & 3) * W4_SLOT;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bf[r][j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 64);
+    };
+    auto read_a = [&](int ks, int r) {
+        const char* sb = smem + (ks & 3) * W4_SLOT;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[r][i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 64);
+    };
+    auto read_frags = [&](int ks, int r) { read_b(ks, r); read_a(ks, r); };
+    // inline-asm MFMA with the accumulator pinned in place in AGPRs ("+a"): with the builtin,
+    // hipcc shuffles part of the 256 accumulators between AGPRs and VGPRs every step
+    auto mfma_rows = [&](int r, int i0, int i1) {
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                             : "+a"(acc[i][j]) : "v"(bf[r][j]), "v"(af[r][i]));
+    };
+
+    stage(0);
+    stage(1);
+    stage(2);
+    stage(3);
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    barrier();
+    read_frags(0, 0);
+    // one step: DMA(st+1) landed (st+2, st+3 in flight) -> barrier -> DMA(st+4) into st's slot ->
+    // next fragments in two batches of 8 under this step's MFMAs (lgkmcnt encodes <= 15)
+    auto step = [&](int st, int u) {
+        // DMA(st+1) landed; this wave's reads of slot st (frags(st), issued last step) are done,
+        // so after the barrier nobody reads slot st and DMA(st+4) may overwrite it
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+        barrier();
+        stage(st + 4);
+        read_b(st + 1, u ^ 1);
+        mfma_rows(u, 0, 4);
+        read_a(st + 1, u ^ 1);
+        mfma_rows(u, 4, 8);
+    };
+    for (int s0 = 0; s0 < ns - 2; s0 += 2) {   // uniform body: the register set is a constant
+        step(s0, 0);
+        step(s0 + 1, 1);
+    }
+    step(ns - 2, 0);
+    mfma_rows(1, 0, 8);
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
 int g_sched = -1;
 int gemm_sched() {
     if (g_sched < 0) {
         const char* e = getenv("CE_GEMM_SCHED");
         g_sched = e ? atoi(e) : 1;
-        if (!(g_sched == 0 || g_sched == 1 || g_sched == 3 || g_sched == 4 || g_sched == 6 || g_sched == 7 ||
-              g_sched == 9))
+        if (!(g_sched == 0 || g_sched == 1 || g_sched == 2 || g_sched == 3 || g_sched == 4 || g_sched == 6 ||
+              g_sched == 7 || g_sched == 9))
             g_sched = 1;
     }
     return g_sched;
@@ -716,7 +835,9 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         const int need = ((nwg + 7) / 8) * 8;
         grid = grid < need ? grid : need;
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
-    } else if (sc == 0)
+    } else if (sc == 2)
+        hipLaunchKernelGGL((gemm_bf16_w4<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
+    else if (sc == 0)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     else if (sc == 1)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
@@ -738,7 +859,7 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
 int set_gemm_schedule(int v) {
     const int prev = gemm_sched() | (gemm_groupm() << 8);
     const int sc = v & 0xff, gm = (v >> 8) & 0xff;
-    g_sched = (sc == 0 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9) ? sc : 1;
+    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--scheds", default="0,1")
     ap.add_argument("--warm-s", type=float, default=2.0)
+    ap.add_argument("--torch-ref", action="store_true", help="also time torch.matmul (hipBLASLt) per shape")
     ap.add_argument("--only", default="", help="comma list of shape names to run (default all)")
     args = ap.parse_args()
     B = args.batch
@@ -88,6 +89,15 @@ def main():
                 ms = timeit(fn, args.reps)
                 tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
                 res.setdefault(f"{name}/s{sched}", []).append(tf)
+    if args.torch_ref:
+        # library reference point: torch.matmul (hipBLASLt) on the same shapes, bf16 out, no epilogue
+        for name, (M, N, K, act, resid, ob) in shapes.items():
+            A, W, bias, R, O = bufs[name]
+            Ob = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            for rnd in range(args.rounds):
+                ms = timeit(lambda: torch.matmul(A, W.t(), out=Ob), args.reps)
+                res.setdefault(f"{name}/torch", []).append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
+            del Ob
     attns = {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B)}
     if args.only:
         attns = {k: v for k, v in attns.items() if k in keep}
