@@ -17,7 +17,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(gemm_bf16_nt|attn_fwd|layernorm_k|fgemm_k|pacl_pool_k|im2col_k)[^(]*", name)
+    m = re.search(r"(gemm_bf16_\w+|attn_fwd|layernorm_k|fgemm_k|pacl_pool_k|im2col_k)[^(]*", name)
     return m.group(0) if m else name[:40]
 
 
