@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("CLIPEMBED_LIB") or os.path.join(_HERE, "libclipembed.
 
 CE_OK, CE_ERR_INVALID, CE_ERR_HIP, CE_ERR_STATE, CE_ERR_OOM = 0, 1, 2, 3, 4
 CE_F32, CE_BF16, CE_F16, CE_I64, CE_I32 = 0, 1, 2, 3, 4
+CE_PRE_CLIP_BICUBIC, CE_PRE_PACL_BILINEAR_AA = 0, 1
 CE_ACT_GELU_ERF, CE_ACT_QUICK_GELU = 0, 1
 CE_PACL_ONES, CE_PACL_SIGMOID10 = 0, 1
 CE_ROPE_NONE, CE_ROPE_BEFORE, CE_ROPE_AFTER = 0, 1, 2
@@ -80,6 +81,8 @@ _SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p]),
     "ce_sparc_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                               c_int, c_float, c_float, c_float, c_void_p]),
+    "ce_preprocess_images": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                     c_int, c_void_p]),
     "ce_apply_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "ce_set_kernel_timing": (c_int, [c_void_p, c_int]),
     "ce_kernel_stats": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_double), POINTER(c_int64),

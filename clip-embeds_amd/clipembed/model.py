@@ -305,9 +305,12 @@ def create_model(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = N
 def create_model_and_transforms(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = None,
                                 device=None, **kw):
     """Returns (model, preprocess_train, preprocess_val) like open_clip (factory.py:822-958).
-    Image preprocessing is outside the drop-in boundary ('next'): both transforms are
-    None; callers feed normalised [B,3,336,336] tensors."""
-    return create_model(model_name, pretrained, device, **kw), None, None
+    preprocess_val is the device eval transform (clipembed.transforms.image_transform: Pillow-exact
+    bicubic resize, center crop, normalise); preprocess_train (RandomResizedCrop augmentation) is
+    not on the device path and is None."""
+    from .transforms import image_transform
+    model = create_model(model_name, pretrained, device, **kw)
+    return model, None, image_transform(model.cfg.vision.image_size, is_train=False, device=device)
 
 
 def load_checkpoint_file(path: str) -> dict:

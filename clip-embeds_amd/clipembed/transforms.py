@@ -1,0 +1,107 @@
+"""Eval image preprocessing on the device — mirrors the reference's host transforms.
+
+  image_transform(336, is_train=False)   open_clip/src/open_clip/transform.py:274-389 (eval path,
+                                         resize_mode 'shortest', bicubic): Resize -> CenterCrop ->
+                                         ToTensor -> Normalize(OpenAI)
+  prepare_data(...).preprocess_image     Patch-Aligned-Contrastive-Learning/data/utils.py:30-52:
+                                         ToTensor -> Resize((S,S)) -> Normalize(ImageNet)
+
+Both run in libclipembed (ce_preprocess_images); the CLIP path reproduces Pillow's fixed-point
+bicubic resampler bit for bit.  Inputs: PIL images, uint8 HWC numpy arrays or uint8 HWC tensors
+(RGB), one at a time (-> [3,S,S], as the reference's transform) or a list (-> [B,3,S,S] in one
+launch).  JPEG/PNG decoding stays on the host.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .model import _ptr, _stream, kernel_engine
+
+
+def _as_hwc_u8(img) -> np.ndarray:
+    if isinstance(img, torch.Tensor):
+        a = img.detach().cpu().numpy()
+    elif isinstance(img, np.ndarray):
+        a = img
+    else:  # PIL.Image (convert('RGB') as _convert_to_rgb, transform.py:238-239)
+        a = np.asarray(img.convert("RGB"))
+    if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError(f"expected an RGB uint8 HWC image, got dtype {a.dtype} shape {a.shape}")
+    return np.ascontiguousarray(a)
+
+
+class DeviceImageProcessor:
+    """Callable like the reference's torchvision Compose; output on the device."""
+
+    def __init__(self, mode: int, image_size: int = 336, device=None, out_dtype=torch.float32, engine=None):
+        if image_size != 336 and engine is None:
+            raise ValueError("the default kernel handle is configured for 336-pixel inputs; pass an engine")
+        self.mode = mode
+        self.image_size = image_size
+        self.device = torch.device(device) if device is not None else None   # None: current device at call
+        self.out_dtype = out_dtype
+        self.engine = engine
+
+    def __call__(self, image):
+        batch = isinstance(image, (list, tuple))
+        imgs = [_as_hwc_u8(x) for x in (image if batch else [image])]
+        out = self.batch(imgs)
+        return out if batch else out[0]
+
+    @torch.no_grad()
+    def batch(self, imgs: Sequence[np.ndarray]) -> torch.Tensor:
+        dev = self.device if self.device is not None else torch.device("cuda", torch.cuda.current_device())
+        e = self.engine if self.engine is not None else kernel_engine(dev)
+        sizes = [x.nbytes for x in imgs]
+        offsets = np.zeros(len(imgs), np.int64)
+        offsets[1:] = np.cumsum(sizes)[:-1]
+        host = torch.empty(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
+        hv = host.numpy()
+        for x, o in zip(imgs, offsets):
+            hv[o:o + x.nbytes] = x.reshape(-1)
+        dev = host.to(e.device, non_blocking=True)
+        heights = np.array([x.shape[0] for x in imgs], np.int32)
+        widths = np.array([x.shape[1] for x in imgs], np.int32)
+        S = self.image_size
+        out = torch.empty(len(imgs), 3, S, S, device=e.device, dtype=self.out_dtype)
+        dt = _lib.CE_BF16 if self.out_dtype == torch.bfloat16 else _lib.CE_F32
+        _lib.call("ce_preprocess_images", e.h, _stream(e.device), _ptr(dev), offsets.ctypes.data,
+                  heights.ctypes.data, widths.ctypes.data, len(imgs), self.mode, dt, _ptr(out))
+        dev.record_stream(torch.cuda.current_stream(e.device))
+        return out
+
+
+def image_transform(image_size=336, is_train: bool = False, mean: Optional[Sequence[float]] = None,
+                    std: Optional[Sequence[float]] = None, resize_mode: Optional[str] = None,
+                    interpolation: Optional[str] = None, fill_color: int = 0, aug_cfg=None, device=None,
+                    engine=None):
+    """open_clip image_transform (transform.py:274-389), eval path on the device."""
+    if isinstance(image_size, (tuple, list)):
+        if image_size[0] != image_size[1]:
+            raise NotImplementedError("non-square image_size (ResizeKeepRatio) is not on the device path")
+        image_size = image_size[0]
+    if is_train:
+        raise NotImplementedError("training augmentations (RandomResizedCrop, jitter) are not on the device path")
+    if (resize_mode or "shortest") != "shortest" or (interpolation or "bicubic") != "bicubic":
+        raise NotImplementedError("only resize_mode='shortest' with bicubic interpolation is on the device path")
+    from .weights import OPENAI_MEAN, OPENAI_STD
+    if (mean is not None and tuple(mean) != tuple(OPENAI_MEAN)) or (std is not None and tuple(std) != tuple(OPENAI_STD)):
+        raise NotImplementedError("the device path normalises with the OpenAI mean/std (constants.py:1-2)")
+    return DeviceImageProcessor(_lib.CE_PRE_CLIP_BICUBIC, image_size, device, engine=engine)
+
+
+class prepare_data:
+    """PACL prepare_data (data/utils.py:30-52): preprocess_image on the device.  The tokenizer half
+    (open_clip get_tokenizer) stays on the host and is not provided here."""
+
+    def __init__(self, base_model: str = "ViT-L-14-336", device=None, engine=None):
+        if base_model != "ViT-L-14-336":
+            raise NotImplementedError("only the ViT-L-14-336 (336 px) pipeline is on the device path")
+        self.val_transform = DeviceImageProcessor(_lib.CE_PRE_PACL_BILINEAR_AA, 336, device, engine=engine)
+
+    def preprocess_image(self, image):
+        return self.val_transform(image)     # a list -> one batched launch, as torch.stack of the reference

@@ -139,6 +139,14 @@ struct ce_handle {
     char* tmp = nullptr;
     size_t tmp_bytes = 0;
     float* scratch = nullptr;    // 256 B
+    // device preprocessing: tap tables (pinned host staging -> device), intermediate rows
+    char* prep_host = nullptr;
+    size_t prep_host_bytes = 0;
+    char* prep_dev = nullptr;
+    size_t prep_dev_bytes = 0;
+    char* prep_tmp = nullptr;
+    size_t prep_tmp_bytes = 0;
+    hipEvent_t prep_ev = nullptr;    // the staging buffer's last upload
     // RoPE tables (pacl.py:147-181): [P][D/2] for D = vision width and D = pacl_dim
     float *rc_v = nullptr, *rs_v = nullptr, *rc_p = nullptr, *rs_p = nullptr;
     // timing
@@ -605,6 +613,10 @@ int ce_destroy(ce_handle* h) {
     if (h->ws_t) (void)hipFree(h->ws_t);
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->scratch) (void)hipFree(h->scratch);
+    if (h->prep_host) (void)hipHostFree(h->prep_host);
+    if (h->prep_dev) (void)hipFree(h->prep_dev);
+    if (h->prep_tmp) (void)hipFree(h->prep_tmp);
+    if (h->prep_ev) (void)hipEventDestroy(h->prep_ev);
     for (float* p : {h->rc_v, h->rs_v, h->rc_p, h->rs_p})
         if (p) (void)hipFree(p);
     for (auto& p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
@@ -1036,6 +1048,208 @@ int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float*
     CE_TRY(check_launch(ce::launch_sparc_local(part, S, mask, B, T, s), "sparc_loss local"));
     return check_launch(ce::launch_sparc_loss_finish(out_loss, lr, lc, part, B, global_weight, local_weight, s),
                         "sparc_loss finish");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Device preprocessing (preprocess.hip).  Tap tables are built here exactly as the reference's
+// third-party resamplers build them: Pillow's precompute_coeffs + normalize_coeffs_8bpc (double
+// precision, 22-bit fixed point) for the CLIP bicubic path, ATen's _compute_weights_aa (float,
+// with its double-precision intermediates) for the PACL antialiased-bilinear path.
+namespace {
+
+double pil_bicubic(double x) {
+    const double a = -0.5;
+    if (x < 0.0) x = -x;
+    if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+    if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+    return 0.0;
+}
+
+// Taps of output indices [o0, o0 + n) of an in_size -> out_size resize; bounds are (start, count)
+// with start shifted by -shift.  Returns the tap row stride.
+int pil_taps(int in_size, int out_size, int o0, int n, int shift, std::vector<int>& bounds, std::vector<int>& taps) {
+    if (in_size == out_size) {            // Pillow skips the pass: identity taps reproduce it exactly
+        for (int i = 0; i < n; ++i) {
+            bounds.push_back(o0 + i - shift);
+            bounds.push_back(1);
+            taps.push_back(1 << 22);
+        }
+        return 1;
+    }
+    const double scale = (double)((float)in_size - 0.0f) / out_size;
+    const double filterscale = scale < 1.0 ? 1.0 : scale;
+    const double support = 2.0 * filterscale;
+    const int ksize = (int)std::ceil(support) * 2 + 1;
+    std::vector<double> k(ksize);
+    for (int i = 0; i < n; ++i) {
+        const int xx = o0 + i;
+        const double center = 0.0 + (xx + 0.5) * scale;
+        const double ss = 1.0 / filterscale;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > in_size) xmax = in_size;
+        xmax -= xmin;
+        double ww = 0.0;
+        for (int x = 0; x < xmax; ++x) {
+            k[x] = pil_bicubic((x + xmin - center + 0.5) * ss);
+            ww += k[x];
+        }
+        for (int x = 0; x < ksize; ++x) {
+            double v = x < xmax ? (ww != 0.0 ? k[x] / ww : k[x]) : 0.0;
+            taps.push_back(v < 0 ? (int)(-0.5 + v * (1 << 22)) : (int)(0.5 + v * (1 << 22)));
+        }
+        bounds.push_back(xmin - shift);
+        bounds.push_back(xmax);
+    }
+    return ksize;
+}
+
+int aa_taps(int in_size, int out_size, int shift, std::vector<int>& bounds, std::vector<float>& taps) {
+    if (in_size == out_size) {            // ATen skips the dimension
+        for (int i = 0; i < out_size; ++i) {
+            bounds.push_back(i - shift);
+            bounds.push_back(1);
+            taps.push_back(1.0f);
+        }
+        return 1;
+    }
+    const float scale = (float)in_size / (float)out_size;
+    const float support = scale >= 1.0f ? scale : 1.0f;
+    const float invscale = scale >= 1.0f ? (float)(1.0 / (double)scale) : 1.0f;
+    const int ksize = (int)std::ceil((double)support) * 2 + 1;
+    std::vector<float> w(ksize);
+    for (int i = 0; i < out_size; ++i) {
+        const float center = (float)((double)scale * (i + 0.5));
+        int xmin = (int)((double)(center - support) + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xs = (int)((double)(center + support) + 0.5);
+        if (xs > in_size) xs = in_size;
+        xs -= xmin;
+        float tot = 0.0f;
+        for (int j = 0; j < xs; ++j) {
+            float t = (float)(((double)((float)(j + xmin) - center) + 0.5) * (double)invscale);
+            if (t < 0) t = -t;
+            w[j] = t < 1.0f ? 1.0f - t : 0.0f;
+            tot += w[j];
+        }
+        for (int j = 0; j < ksize; ++j) taps.push_back(j < xs ? (tot != 0.0f ? w[j] / tot : w[j]) : 0.0f);
+        bounds.push_back(xmin - shift);
+        bounds.push_back(xs);
+    }
+    return ksize;
+}
+
+int grow_pinned(char*& buf, size_t& bytes, size_t need) {
+    if (need <= bytes) return CE_OK;
+    if (buf) HIP_TRY(hipHostFree(buf));
+    buf = nullptr;
+    bytes = 0;
+    if (hipHostMalloc((void**)&buf, need) != hipSuccess) {
+        buf = nullptr;
+        (void)hipGetLastError();
+        return fail(CE_ERR_OOM, "cannot allocate %zu bytes of pinned staging", need);
+    }
+    bytes = need;
+    return CE_OK;
+}
+
+}  // namespace
+
+int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
+                         const int* heights, const int* widths, int B, int mode, int out_dtype, void* out) {
+    if (!h || !images || !offsets || !heights || !widths || !out)
+        return fail(CE_ERR_INVALID, "ce_preprocess_images: null argument");
+    if (B <= 0) return fail(CE_ERR_INVALID, "ce_preprocess_images: batch must be positive (got %d)", B);
+    if (mode != CE_PRE_CLIP_BICUBIC && mode != CE_PRE_PACL_BILINEAR_AA)
+        return fail(CE_ERR_INVALID, "ce_preprocess_images: unknown mode %d", mode);
+    if (out_dtype != CE_F32 && out_dtype != CE_BF16)
+        return fail(CE_ERR_INVALID, "ce_preprocess_images: output must be f32 or bf16");
+    const int S = h->cfg.image_size;
+    const bool pacl = mode == CE_PRE_PACL_BILINEAR_AA;
+    std::vector<ce::PrepMeta> meta(B);
+    std::vector<int> bounds, itaps;
+    std::vector<float> ftaps;
+    long long tmp_elems = 0;
+    int max_rows = 0;
+    for (int b = 0; b < B; ++b) {
+        const int H = heights[b], Wd = widths[b];
+        if (H <= 0 || Wd <= 0 || offsets[b] < 0)
+            return fail(CE_ERR_INVALID, "ce_preprocess_images: image %d has bad size %dx%d", b, H, Wd);
+        ce::PrepMeta& m = meta[b];
+        m.in_off = offsets[b];
+        m.H = H;
+        m.W = Wd;
+        m.bx_off = (int)bounds.size();
+        if (!pacl) {
+            // torchvision Resize(S) shortest edge (_compute_resized_output_size) + CenterCrop(S)
+            // offsets int(round(d / 2.0)) with round-half-even
+            const bool wshort = Wd <= H;
+            const int sh = wshort ? Wd : H, lg = wshort ? H : Wd;
+            const int nl = (int)((double)S * lg / sh);
+            const int nw = wshort ? S : nl, nh = wshort ? nl : S;
+            const int top = (int)std::nearbyint((nh - S) / 2.0), left = (int)std::nearbyint((nw - S) / 2.0);
+            m.kx_off = (int)itaps.size();
+            m.ksx = pil_taps(Wd, nw, left, S, 0, bounds, itaps);
+            // vertical taps first into scratch to learn the source row window
+            std::vector<int> vb, vt;
+            const int ksy = pil_taps(H, nh, top, S, 0, vb, vt);
+            m.ybase = vb[0];
+            m.nrows = vb[2 * (S - 1)] + vb[2 * (S - 1) + 1] - m.ybase;
+            for (int i = 0; i < S; ++i) vb[2 * i] -= m.ybase;
+            m.by_off = (int)bounds.size();
+            bounds.insert(bounds.end(), vb.begin(), vb.end());
+            m.ky_off = (int)itaps.size();
+            m.ksy = ksy;
+            itaps.insert(itaps.end(), vt.begin(), vt.end());
+        } else {
+            m.kx_off = (int)ftaps.size();
+            m.ksx = aa_taps(Wd, S, 0, bounds, ftaps);
+            std::vector<int> vb;
+            std::vector<float> vt;
+            const int ksy = aa_taps(H, S, 0, vb, vt);
+            m.ybase = vb[0];
+            m.nrows = vb[2 * (S - 1)] + vb[2 * (S - 1) + 1] - m.ybase;
+            for (int i = 0; i < S; ++i) vb[2 * i] -= m.ybase;
+            m.by_off = (int)bounds.size();
+            bounds.insert(bounds.end(), vb.begin(), vb.end());
+            m.ky_off = (int)ftaps.size();
+            m.ksy = ksy;
+            ftaps.insert(ftaps.end(), vt.begin(), vt.end());
+        }
+        m.tmp_off = tmp_elems;
+        tmp_elems += (long long)m.nrows * S * 3;
+        if (m.nrows > max_rows) max_rows = m.nrows;
+    }
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t meta_b = (size_t)B * sizeof(ce::PrepMeta);
+    const size_t bounds_b = bounds.size() * 4;
+    const size_t taps_b = pacl ? ftaps.size() * 4 : itaps.size() * 4;
+    const size_t total = meta_b + bounds_b + taps_b;
+    if (h->prep_ev) HIP_TRY(hipEventSynchronize(h->prep_ev));     // staging buffer free again
+    else HIP_TRY(hipEventCreateWithFlags(&h->prep_ev, hipEventDisableTiming));
+    CE_TRY(grow_pinned(h->prep_host, h->prep_host_bytes, total));
+    CE_TRY(grow_buffer(h->prep_dev, h->prep_dev_bytes, total));
+    CE_TRY(grow_buffer(h->prep_tmp, h->prep_tmp_bytes, (size_t)tmp_elems * (pacl ? 4 : 1)));
+    memcpy(h->prep_host, meta.data(), meta_b);
+    memcpy(h->prep_host + meta_b, bounds.data(), bounds_b);
+    memcpy(h->prep_host + meta_b + bounds_b, pacl ? (const void*)ftaps.data() : (const void*)itaps.data(), taps_b);
+    HIP_TRY(hipMemcpyAsync(h->prep_dev, h->prep_host, total, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(h->prep_ev, s));
+    static const float kOpenaiMean[3] = {0.48145466f, 0.4578275f, 0.40821073f};
+    static const float kOpenaiStd[3] = {0.26862954f, 0.26130258f, 0.27577711f};
+    static const float kImagenetMean[3] = {0.485f, 0.456f, 0.406f};
+    static const float kImagenetStd[3] = {0.229f, 0.224f, 0.225f};
+    return timed(h, s, "preprocess", 0.0, (double)tmp_elems * 2 + (double)B * 3 * S * S * (out_dtype == CE_BF16 ? 2 : 4),
+                 [&] {
+                     return ce::launch_preprocess(images, (const ce::PrepMeta*)h->prep_dev,
+                                                  (const int*)(h->prep_dev + meta_b),
+                                                  (const void*)(h->prep_dev + meta_b + bounds_b), h->prep_tmp, B,
+                                                  max_rows, S, pacl, out_dtype == CE_BF16,
+                                                  pacl ? kImagenetMean : kOpenaiMean, pacl ? kImagenetStd : kOpenaiStd,
+                                                  out, s);
+                 });
 }
 
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out) {

@@ -100,4 +100,21 @@ hipError_t launch_sparc_local(float* part, const float* S, const float* mask, in
 hipError_t launch_sparc_loss_finish(float* out, const float* lr, const float* lc, const float* part, int B,
                                     float global_weight, float local_weight, hipStream_t s);
 
+// Device image preprocessing (preprocess.hip).  Per image: source offset/size, the source rows
+// the vertical taps touch [ybase, ybase + nrows), the intermediate's offset, and tap tables:
+// bounds (start, count) pairs at bx_off (S output columns, absolute source x) and by_off (S output
+// rows, relative to ybase); taps (int32 Pillow fixed point, or f32) at kx_off / ky_off with row
+// strides ksx / ksy.
+struct PrepMeta {
+    long long in_off;
+    int H, W;
+    int ybase, nrows;
+    long long tmp_off;
+    int bx_off, by_off;
+    int kx_off, ksx, ky_off, ksy;
+};
+hipError_t launch_preprocess(const uint8_t* images, const PrepMeta* meta, const int* bounds, const void* taps,
+                             void* tmp, int B, int max_rows, int S, bool pacl, bool out_bf16, const float* mean,
+                             const float* stdv, void* out, hipStream_t s);
+
 }  // namespace ce

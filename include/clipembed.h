@@ -194,6 +194,21 @@ int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l,
                      int T, int D, float sigma, float* out_grouped, float* out_l_norm,
                      float* out_sim);
 
+/* Eval image preprocessing on the device, replacing the host-side pipelines:
+ *   CE_PRE_CLIP_BICUBIC     open_clip/src/open_clip/transform.py:371-389 (image_transform, eval,
+ *                           resize_mode 'shortest'): Resize(S, BICUBIC) of the shortest edge with
+ *                           Pillow's fixed-point resampler (bit-exact), CenterCrop(S), ToTensor,
+ *                           Normalize(OpenAI mean/std, constants.py:1-2)
+ *   CE_PRE_PACL_BILINEAR_AA Patch-Aligned-Contrastive-Learning/data/utils.py:33-37: ToTensor,
+ *                           Resize((S,S)) bilinear with antialias on the float tensor
+ *                           (torch interpolate), Normalize(ImageNet mean/std)
+ * images: device uint8 RGB, image b is HWC [heights[b]][widths[b]][3] at images + offsets[b];
+ * offsets / heights / widths are HOST arrays of B entries.  S = cfg.image_size.
+ * out: device [B,3,S,S] f32 or bf16 (out_dtype), ready for ce_encode_image. */
+enum ce_preprocess_mode { CE_PRE_CLIP_BICUBIC = 0, CE_PRE_PACL_BILINEAR_AA = 1 };
+int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
+                         const int* heights, const int* widths, int B, int mode, int out_dtype, void* out);
+
 /* SparcLoss.forward (Patch-Aligned-Contrastive-Learning/model/pacl.py:564-584, masked local loss
  * :527-562): global_weight (reference 0.5, :520) * CLIP loss (logit scale 1/temperature) of the
  * L2-normalised means of v_patch over P and of l_tokens over T, + local_weight (reference 1.0,
