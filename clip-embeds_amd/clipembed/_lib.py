@@ -85,11 +85,13 @@ _SIGNATURES = {
                                      c_int, c_void_p]),
     "ce_apply_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "ce_set_kernel_timing": (c_int, [c_void_p, c_int]),
+    "ce_set_kernel_timing_filter": (c_int, [c_void_p, c_char_p]),
     "ce_kernel_stats": (c_int, [c_void_p, c_int, c_char_p, c_int, POINTER(c_double), POINTER(c_int64),
                                 POINTER(c_double), POINTER(c_double)]),
     "ce_kernel_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                     c_void_p, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),
+    "ce_set_gemm_splitk": (c_int, [c_int]),
     "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
     "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
 }

@@ -99,7 +99,9 @@ class Engine:
         return n.value, (first.value or b"").decode()
 
     # ---- timing (roofline reporting) ----
-    def set_timing(self, on: bool):
+    def set_timing(self, on: bool, only: str = ""):
+        """Bracket kernel launches with HIP events (all tags, or only the launches tagged `only`)."""
+        _lib.call("ce_set_kernel_timing_filter", self.h, only.encode())
         _lib.call("ce_set_kernel_timing", self.h, 1 if on else 0)
 
     def kernel_stats(self):

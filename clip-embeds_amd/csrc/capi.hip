@@ -151,6 +151,8 @@ struct ce_handle {
     float *rc_v = nullptr, *rs_v = nullptr, *rc_p = nullptr, *rs_p = nullptr;
     // timing
     bool timing = false;
+    std::string timing_only;     // non-empty: only launches with this tag are bracketed
+    float* cur_part = nullptr;   // GEMM split-K slabs of the tower whose launches are being issued
     std::vector<KStat> stats;
     std::map<std::string, int> stat_idx;
     std::vector<Pending> pending;
@@ -289,7 +291,7 @@ hipEvent_t get_event(ce_handle* h) {
 
 template <class F>
 int timed(ce_handle* h, hipStream_t s, const char* name, double flops, double bytes, F&& launch) {
-    if (!h->timing) {
+    if (!h->timing || (!h->timing_only.empty() && h->timing_only != name)) {
         hipError_t e = launch();
         if (e != hipSuccess) return fail(CE_ERR_HIP, "%s launch failed: %s", name, hipGetErrorString(e));
         return CE_OK;
@@ -329,6 +331,8 @@ struct TowerWs {
     bf16_t *xn, *qkv, *att, *hid;
     float* pooled;
     int* rows;
+    float* part;     // GEMM split-K partial tiles (ce::kGemmPartElems f32), per tower: the towers may
+                     // run concurrently on two streams
 };
 
 size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
@@ -340,6 +344,7 @@ size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
     n += align256(std::max(rows * F, extra_hid_elems) * 2);
     n += align256(B * D * 4);
     n += align256(B * 4);
+    n += align256(ce::kGemmPartElems * 4);
     return n;
 }
 
@@ -352,7 +357,8 @@ TowerWs carve(char* base, long rows, int D, int F, long extra_hid_elems, long B)
     w.att = (bf16_t*)p; p += align256(rows * D * 2);
     w.hid = (bf16_t*)p; p += align256(std::max(rows * F, extra_hid_elems) * 2);
     w.pooled = (float*)p; p += align256(B * D * 4);
-    w.rows = (int*)p;
+    w.rows = (int*)p; p += align256(B * 4);
+    w.part = (float*)p;
     return w;
 }
 
@@ -408,6 +414,8 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.resid = resid; p.ldr = N;
     p.out = out; p.ldo = N;
     p.grp = grp; p.o_gs = o_gs; p.o_go = o_go; p.r_gs = r_gs; p.r_go = r_go;
+    p.part = h->cur_part;            // split-K tail slabs of the tower being run (null: no split)
+    p.part_elems = h->cur_part ? ce::kGemmPartElems : 0;
     const double flops = 2.0 * M * N * K;
     const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
                          (resid ? (double)M * N * 4 : 0.0);
@@ -433,6 +441,11 @@ int act_code(const ce_handle* h) { return h->cfg.activation == CE_ACT_QUICK_GELU
 int run_block(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, int B, int L, int D, int H,
               int F, bool causal, bool vis) {
     const int M = B * L;
+    struct PartScope {      // split-K slabs of this tower for the block's GEMMs, cleared on every exit
+        ce_handle* h;
+        ~PartScope() { h->cur_part = nullptr; }
+    } scope{h};
+    h->cur_part = w.part;
     CE_TRY(layernorm(h, s, vis ? "ln_v" : "ln_t", w.x, w.xn, true, k.ln1w, k.ln1b, M, D));
     CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, k.wqkv, M, 3 * D, D, k.bqkv, ce::ACT_NONE_,
                 nullptr, w.qkv, true));
@@ -1276,6 +1289,12 @@ int ce_set_kernel_timing(ce_handle* h, int enable) {
     return CE_OK;
 }
 
+int ce_set_kernel_timing_filter(ce_handle* h, const char* tag) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_set_kernel_timing_filter: null handle");
+    h->timing_only = tag ? tag : "";
+    return CE_OK;
+}
+
 int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* total_ms, int64_t* launches,
                     double* flops, double* bytes) {
     if (!h) return fail(CE_ERR_INVALID, "ce_kernel_stats: null handle");
@@ -1304,10 +1323,12 @@ int ce_kernel_gemm_bf16(void* stream, const void* A, const void* Wt, int M, int 
     ce::GemmParams p{};
     p.A = (const bf16_t*)A; p.lda = K; p.W = (const bf16_t*)Wt; p.ldw = K;
     p.M = M; p.N = N; p.K = K; p.bias = bias; p.resid = resid; p.ldr = N; p.out = out; p.ldo = N;
+    p.part = ce::gemm_kernel_api_workspace(&p.part_elems);
     return check_launch(ce::launch_gemm(p, act, out_dtype == CE_BF16, (hipStream_t)stream), "gemm");
 }
 
 int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
+int ce_set_gemm_splitk(int enable) { return ce::set_gemm_splitk(enable); }
 
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal) {
     if (!qkv || !out) return fail(CE_ERR_INVALID, "ce_kernel_attention: null argument");

@@ -22,9 +22,16 @@ struct GemmParams {
     void* out; long ldo;               // f32 or bf16
     int grp, o_gs, o_go, r_gs, r_go;
     int gm = 0;                        // tile-order M-group (set by launch_gemm)
+    // split-K tail (set by launch_gemm): the last `tail` tiles are computed as `split` K-chunks each
+    // (partial f32 tiles into `part`), summed in fixed order by a fixup kernel
+    float* part = nullptr; long part_elems = 0;
+    int tail = 0, split = 1;
 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s);
 int set_gemm_schedule(int v);   // returns previous
+int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
+float* gemm_kernel_api_workspace(long* elems);   // per-device partial-tile buffer (kernel-level API)
+constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a handle provides (64 MB)
 
 // Multi-head attention over a packed QKV activation.
 //   qkv [B*L][3*D] bf16 (q | k | v, head h at columns h*64 .. h*64+63 of each part)

@@ -22,7 +22,12 @@
 #include "ce_device.h"
 #include "ce_kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
+
+#ifndef CE_RESID_RING
+#define CE_RESID_RING 4
+#endif
 
 namespace ce {
 
@@ -80,7 +85,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int
                                              0x00020000);
 }
 
-template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING>
 __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase,
                                                    int nbase, int lane) {
     const int fr = lane & 15, fq = lane >> 4;
@@ -95,7 +100,10 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
     // 16-column blocks inside N (wave-uniform; N % 64 == 0, so a 64-column slab is whole and only
     // the 128-column slabs of SCHED 2 can be cut)
     const int jmax = NJ > 4 ? min(NJ, (p.N - nbase) / 16) : NJ;
-    float4 rbuf[2][NJ];
+    // residual rows are prefetched RD-1 fragment rows ahead (RD-deep register ring): one HBM latency
+    // per RD-1 rows instead of one per row
+    constexpr int RD = NJ > 4 ? 2 : RING;
+    float4 rbuf[RD][NJ];
     auto load_resid = [&](int i, float4 (&r)[NJ]) {
         int m = mbase + i * 16 + fr;
         if constexpr (CHECK_M) m = m < p.M ? m : p.M - 1;     // clamp: a valid row, result unused
@@ -104,12 +112,15 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         for (int j = 0; j < NJ; ++j)
             if (j < jmax) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
     };
-    if constexpr (HAS_RESID) load_resid(0, rbuf[0]);
+    if constexpr (HAS_RESID) {
+#pragma unroll
+        for (int i = 0; i < RD - 1; ++i) load_resid(i, rbuf[i]);
+    }
     uint2 pend[NJ];      // bf16 output: packed values of the even fragment row, awaiting its partner
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         if constexpr (HAS_RESID) {
-            if (i + 1 < 8) load_resid(i + 1, rbuf[(i + 1) & 1]);
+            if (i + RD - 1 < 8) load_resid(i + RD - 1, rbuf[(i + RD - 1) % RD]);
         }
         const int m = mbase + i * 16 + fr;
         if constexpr (CHECK_M && !OUT_BF16) {
@@ -129,7 +140,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                 v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
             }
             if constexpr (HAS_RESID) {
-                const float4 rr = rbuf[i & 1][j];
+                const float4 rr = rbuf[i % RD][j];
                 v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
             }
             if constexpr (OUT_BF16) {
@@ -170,14 +181,14 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
 // fragment row i+1 are issued before the stores of row i (two-deep register ring).  Column slabs
 // are whole (N % 64 == 0), so the only bounds check is on rows, and only in the last M tile: the
 // interior path has no divergent branch, which keeps hipcc's waitcnt counting exact.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int NJ = 4>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int NJ = 4, int RING = CE_RESID_RING>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase, int nbase,
                                               int lane) {
     if (nbase >= p.N) return;                                   // wave-uniform
     if (mbase + 128 <= p.M)
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false, NJ>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false, NJ, RING>(p, acc, mbase, nbase, lane);
     else
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true, NJ>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true, NJ, RING>(p, acc, mbase, nbase, lane);
 }
 
 
@@ -490,7 +501,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_persist(GemmParams p) {
 //          W rows of quadrant-col nh}, each double-buffered; phase p computes one 64x32
 //          quadrant of every wave's 128x64 output (16 MFMAs) and issues the LDS-DMA of one
 //          half-tile of K-tile t+1, so every load has ~3 phases to land; one barrier per phase.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED, int RING = CE_RESID_RING>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
@@ -505,8 +516,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int tiles_n = (p.N + BN - 1) / BN;
     const int nwg = tiles_m * tiles_n;
     const int bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int nk = p.K / BK;
+    // split-K tail (SCHED 1): blocks past t_main (dispatched last, so they fill the final, otherwise
+    // mostly idle round of the grid) each take one K-chunk of one of the last `tail` tiles
+    const int t_main = nwg - (SCHED == 1 ? p.tail : 0);
+    int wgid, kt0 = 0, kt1 = nk, slab = -1;
+    if (bid < t_main) {
+        wgid = xcd_remap(bid, t_main);
+    } else {
+        slab = bid - t_main;
+        const int c = slab % p.split;
+        wgid = t_main + slab / p.split;
+        kt0 = c * nk / p.split;
+        kt1 = (c + 1) * nk / p.split;
+    }
     int tm, tn;
     tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
@@ -521,8 +544,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = p.K / BK;
 
     if constexpr (SCHED == 0) {
         // ---- staging addresses: thread -> (row tid>>3 of a 64-row pass, 16-B chunk) -----
@@ -623,12 +644,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
         const int a_off = wm * 128 * 128;
         const int w_off = TILE_BYTES + wn * 64 * 128;
 
-        // prologue: K-tile 0, issue order A0, B0, B1, A1 (same as the steady-state phases)
-        stageA(0, 0, 0);
-        stageB(0, 0, 0);
-        stageB(0, 0, 1);
-        stageA(0, 0, 1);
-        if (nk > 1) wait_vm_if<WAITS>(4); else wait_vm_if<WAITS>(0);
+        // prologue: K-tile kt0, issue order A0, B0, B1, A1 (same as the steady-state phases)
+        stageA(kt0, 0, 0);
+        stageB(kt0, 0, 0);
+        stageB(kt0, 0, 1);
+        stageA(kt0, 0, 1);
+        if (kt1 - kt0 > 1) wait_vm_if<WAITS>(4); else wait_vm_if<WAITS>(0);
         barrier_if<BARS>();
 
         bf16x8 af[4][2], bfr[2][2];
@@ -664,9 +685,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
             mfma_half(mh, nh, 0);
             mfma_half(mh, nh, 1);
         };
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = kt & 1, nxt = cur ^ 1;
-            const bool more = kt + 1 < nk;
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const int cur = (kt - kt0) & 1, nxt = cur ^ 1;
+            const bool more = kt + 1 < kt1;
             const char* sb = smem + cur * STAGE_BYTES;
             // phase 1: quadrant (0,0); prefetch HA0(t+1)
             readA(sb, 0);
@@ -691,7 +712,56 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
         }
     }
 
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+    if (SCHED == 1 && slab >= 0) {
+        // split-K tail chunk: raw f32 partial tile, row-major [256][256], slab `slab` of p.part
+        float* dst = p.part + (size_t)slab * (BM * BN) + (size_t)(wm * 128 + fr) * BN + wn * 64 + fq * 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<f32x4*>(dst + (size_t)i * 16 * BN + j * 16) = acc[i][j];
+        return;
+    }
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, RING>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+}
+
+// Split-K tail fixup: sums the `split` partial slabs of each tail tile in fixed order (deterministic)
+// and applies the epilogue (bias, activation, residual, f32/bf16 store).  One thread per 4 columns
+// of one row; 64 blocks of 256 threads per tile.
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
+    const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+    const int t_main = tiles_m * tiles_n - p.tail;
+    const int r = blockIdx.x >> 6;
+    const int e = ((blockIdx.x & 63) << 8) + threadIdx.x;     // float4 index inside the 256x256 tile
+    const int row = e >> 6, c4 = (e & 63) * 4;
+    int tm, tn;
+    tile_of(t_main + r, tiles_m, tiles_n, p.gm, tm, tn);
+    const int m = tm * BM + row, n = tn * BN + c4;
+    if (m >= p.M || n >= p.N) return;
+    const float* src = p.part + (size_t)r * p.split * (BM * BN) + (size_t)row * BN + c4;
+    f32x4 v = *reinterpret_cast<const f32x4*>(src);
+    for (int c = 1; c < p.split; ++c) v += *reinterpret_cast<const f32x4*>(src + (size_t)c * (BM * BN));
+    if (p.bias) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if constexpr (ACT == ACT_GELU) {
+        const f32x2 lo = gelu_pair(f32x2{v[0], v[1]}), hi = gelu_pair(f32x2{v[2], v[3]});
+        v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+    } else {
+        v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
+        v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
+    }
+    if constexpr (HAS_RESID) {
+        const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + n);
+        v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
+    }
+    const size_t o = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + n;
+    if constexpr (OUT_BF16)
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    else
+        *reinterpret_cast<float4*>(static_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -810,6 +880,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4(GemmParams p) {
 }
 
 int g_sched = -1;
+int g_ring = CE_RESID_RING;     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
 int gemm_sched() {
     if (g_sched < 0) {
         const char* e = getenv("CE_GEMM_SCHED");
@@ -844,12 +915,66 @@ int gemm_groupm() {
     return g_groupm;
 }
 
+// Split-K tail plan: with one 512-thread workgroup per CU, a grid of T tiles runs in ceil(T / CUs)
+// rounds; when the last round holds only R = T % CUs tiles (vision out-proj / c_proj at B = 256:
+// 2308 tiles = 9 rounds + 4 tiles) the chip idles for most of a tile time.  Those R tiles are split
+// into S K-chunks (R * S <= CUs) so the last round is ~1/S of a tile, plus a tiny fixup launch.
+int g_splitk = -1;
+bool splitk_enabled() {
+    if (g_splitk < 0) {
+        const char* e = getenv("CE_GEMM_SPLITK");
+        g_splitk = e ? (atoi(e) != 0) : 1;
+    }
+    return g_splitk != 0;
+}
+
+void plan_tail(GemmParams& p, int nwg) {
+    p.tail = 0;
+    p.split = 1;
+    const int C = num_cus(), nk = p.K / BK;
+    if (!splitk_enabled() || !p.part || nwg <= C) return;
+    const int R = nwg % C;
+    if (R == 0 || R > C / 32) return;     // measured: R = 4 (out/c_proj) gains 3-5 %, R = 12 (QKV) loses
+    int S = std::min(std::min(nk, 16), C / R);
+    while (S >= 2 && (long)R * S * BM * BN > p.part_elems) --S;
+    if (S < 2) return;
+    p.tail = R;
+    p.split = S;
+}
+
+// Per-device partial-tile workspace for the kernel-level entry point (engine handles pass their own).
+float* g_part[64] = {};
+constexpr long kPartElems = 256L * BM * BN;     // 64 MB: R * S <= 256 slabs
+float* kernel_api_part() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!g_part[dev] && hipMalloc(&g_part[dev], kPartElems * sizeof(float)) != hipSuccess) {
+        (void)hipGetLastError();
+        g_part[dev] = nullptr;
+    }
+    return g_part[dev];
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
     p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const int sc = gemm_sched();
+    p.tail = 0;
+    p.split = 1;
+    if (sc == 1) {
+        plan_tail(p, nwg);
+        if (p.tail > 0) {
+            const int grid = nwg - p.tail + p.tail * p.split;
+            if (HAS_RESID && g_ring == 2)
+                hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(grid), dim3(NTHREADS), 0, s, p);
+            else
+                hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(grid), dim3(NTHREADS), 0, s, p);
+            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
+            return hipGetLastError();
+        }
+    }
     if (sc == 9) {
         // one workgroup per CU (a multiple of 8 so every XCD group is complete)
         int grid = (num_cus() / 8) * 8;
@@ -860,6 +985,12 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         hipLaunchKernelGGL((gemm_bf16_w4<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
     else if (sc == 0)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (sc == 1 && HAS_RESID && g_ring == 2)   // residual prefetch-depth A/B (bench_kernels)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (sc == 1 && HAS_RESID && g_ring == 3)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 3>), dim3(nwg), dim3(NTHREADS), 0, s, p);
+    else if (sc == 1 && HAS_RESID && g_ring == 5)
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 5>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     else if (sc == 1)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     else if (sc == 6)
@@ -877,9 +1008,21 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
 
 }  // namespace
 
+int set_gemm_splitk(int on) {
+    const int prev = splitk_enabled() ? 1 : 0;
+    g_splitk = on != 0;
+    return prev;
+}
+
+float* gemm_kernel_api_workspace(long* elems) {
+    *elems = kPartElems;
+    return kernel_api_part();
+}
+
 int set_gemm_schedule(int v) {
     const int prev = gemm_sched() | (gemm_groupm() << 8);
-    const int sc = v & 0xff, gm = (v >> 8) & 0xff;
+    const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff;
+    if (ring >= 2 && ring <= 5) g_ring = ring;
     g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;

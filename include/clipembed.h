@@ -228,6 +228,9 @@ int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int 
  * / LayerNorm kernels is bracketed by HIP events on its stream and the elapsed times are
  * accumulated per kernel tag.  ce_kernel_stats reads them (after a stream sync). */
 int ce_set_kernel_timing(ce_handle* h, int enable);
+/* Restrict timing to the launches whose tag equals `tag` (NULL or "" = all tags): the bench brackets
+ * only the dominant kernel inside its timed region, so the events do not perturb the step time. */
+int ce_set_kernel_timing_filter(ce_handle* h, const char* tag);
 int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* total_ms,
                     int64_t* launches, double* flops, double* bytes);
 
@@ -241,6 +244,9 @@ int ce_kernel_gemm_bf16(void* stream, const void* A, const void* W, int M, int N
  * ring, 1 = 4-phase half-tile ring, the default; bits 8-15: tile-order M-group, 0 = keep);
  * returns the previous value in the same encoding.  For A/B measurement. */
 int ce_set_gemm_schedule(int schedule);
+/* Split-K tail of the GEMM (default on): when a grid's last round holds few tiles, those tiles are
+ * computed as K-chunks summed by a fixup launch.  Returns the previous setting.  For A/B. */
+int ce_set_gemm_splitk(int enable);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);
 /* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */

@@ -58,6 +58,39 @@ def test_gemm(M, N, K, variant, sched):
     assert err <= tol, f"max err {err} vs tol {tol}"
 
 
+@pytest.mark.parametrize("M,N,K", [(66560, 256, 1024), (66460, 512, 512), (33280, 1024, 4096)])
+@pytest.mark.parametrize("variant", ["gelu_bf16", "resid_f32", "bias_bf16"])
+def test_gemm_splitk_tail(M, N, K, variant):
+    """Grids of 256 * rounds + a few tiles: the last tiles run as K-chunks + a fixup launch.  Checked
+    against the f32 reference and against the same launch with the split disabled."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    resid = torch.randn(M, N, generator=g).to(DEV) if variant == "resid_f32" else None
+    act = 1 if variant == "gelu_bf16" else 0
+    out_bf16 = variant.endswith("bf16")
+    outs = []
+    for split in (1, 0):
+        prev = _lib.lib().ce_set_gemm_splitk(split)
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+        _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), act, P(resid), P(out),
+                  _lib.CE_BF16 if out_bf16 else _lib.CE_F32)
+        torch.cuda.synchronize()
+        _lib.lib().ce_set_gemm_splitk(prev)
+        outs.append(out.float())
+    ref = A.float() @ W.float().t() + bias
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    if resid is not None:
+        ref = ref + resid
+    tol = (2e-2 if out_bf16 else 2e-3) * max(1.0, ref.abs().max().item())
+    for o in outs:
+        assert (o - ref).abs().max().item() < tol
+    # the two paths differ only in the summation order of the tail tiles
+    assert (outs[0] - outs[1]).abs().max().item() < tol
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     n = 256

@@ -53,6 +53,9 @@ def main():
         "qkv_t": (Mt, 2304, 768, 0, False, True), "fc_t": (Mt, 3072, 768, 1, False, True),
         # diagnostics: A resident in L2/MALL (M = 8192) and a square 4096^3 reference point
         "qkv_m8k": (8192, 3072, 1024, 0, False, True), "sq4096": (4096, 4096, 4096, 0, False, True),
+        # epilogue ablations: the vision shapes with a plain bf16 store (no GELU / residual / f32 out)
+        "fc_v_plain": (Mv, 4096, 1024, 0, False, True), "out_v_plain": (Mv, 1024, 1024, 0, False, True),
+        "proj_v_plain": (Mv, 1024, 4096, 0, False, True),
     }
     if args.only:
         keep = set(args.only.split(","))
@@ -77,9 +80,12 @@ def main():
         O = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
         bufs[name] = (A, W, bias, R, O)
     for rnd in range(args.rounds):
-        for sched in args.scheds.split(","):   # "1" or "1g4" (schedule 1, tile-order M-group 4)
-            sc, _, gm = sched.partition("g")
-            _lib.lib().ce_set_gemm_schedule(int(sc) | (int(gm or 0) << 8))   # g0 = keep the default
+        for sched in args.scheds.split(","):   # "1", "1g4" (tile-order M-group 4), "1r3" (resid ring 3),
+            # "1n" (split-K tail off)
+            _lib.lib().ce_set_gemm_splitk(0 if sched.endswith("n") else 1)
+            sc, _, rg = sched.rstrip("n").partition("r")
+            sc, _, gm = sc.partition("g")
+            _lib.lib().ce_set_gemm_schedule(int(sc) | (int(gm or 0) << 8) | (int(rg or 0) << 16))
             for name, (M, N, K, act, resid, ob) in shapes.items():
                 A, W, bias, R, O = bufs[name]
 
