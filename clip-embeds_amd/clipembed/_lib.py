@@ -94,6 +94,14 @@ _SIGNATURES = {
     "ce_set_gemm_splitk": (c_int, [c_int]),
     "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
     "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
+    "ce_tokenizer_create": (c_int, [c_char_p, ctypes.c_size_t, POINTER(c_char_p), c_int, POINTER(c_void_p)]),
+    "ce_tokenizer_destroy": (c_int, [c_void_p]),
+    "ce_tokenizer_last_error": (c_char_p, []),
+    "ce_tokenizer_vocab_size": (c_int, [c_void_p]),
+    "ce_tokenizer_special_ids": (c_int, [c_void_p, POINTER(ctypes.c_int32), POINTER(ctypes.c_int32)]),
+    "ce_tokenizer_encode": (c_int, [c_void_p, c_char_p, c_void_p, c_int, POINTER(c_int)]),
+    "ce_tokenize": (c_int, [c_void_p, POINTER(c_char_p), c_int, c_int, c_void_p]),
+    "ce_tokenizer_decode": (c_int, [c_void_p, c_void_p, c_int, c_char_p, c_int, POINTER(c_int)]),
 }
 
 _lib = None

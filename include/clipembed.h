@@ -22,6 +22,7 @@
 #ifndef CLIPEMBED_H
 #define CLIPEMBED_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -252,6 +253,28 @@ int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, 
 /* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */
 int ce_kernel_layernorm(void* stream, const float* in, void* out, int out_dtype, const float* w,
                         const float* b, int rows, int D);
+
+/* ---- CLIP BPE tokenizer (host; replaces open_clip SimpleTokenizer, tokenizer.py:133-265) ----
+ * `merges` is the DECOMPRESSED text of bpe_simple_vocab_16e6.txt.gz (tokenizer.py:144: header
+ * line, then "a b" merge lines); extra specials follow <start_of_text>, <end_of_text>
+ * (tokenizer.py:151-154).  Text passed in is already cleaned (ftfy / html.unescape / whitespace /
+ * lower: tokenizer.py:66-90 -- done by the Python host layer); UTF-8.  Status 0 = ok, else see
+ * ce_tokenizer_last_error(). */
+typedef struct ce_tokenizer ce_tokenizer;
+int ce_tokenizer_create(const char* merges, size_t len, const char* const* extra_special, int n_extra,
+                        ce_tokenizer** out);
+int ce_tokenizer_destroy(ce_tokenizer* t);
+const char* ce_tokenizer_last_error(void);
+int ce_tokenizer_vocab_size(const ce_tokenizer* t);
+int ce_tokenizer_special_ids(const ce_tokenizer* t, int32_t* sot, int32_t* eot);
+/* SimpleTokenizer.encode (tokenizer.py:213-219): ids of one text, no SOT/EOT.  Writes
+ * min(n, cap) ids; *n_out = n (call with ids = NULL to size the buffer). */
+int ce_tokenizer_encode(ce_tokenizer* t, const char* text, int32_t* ids, int cap, int* n_out);
+/* SimpleTokenizer.__call__ (tokenizer.py:226-265): out[n][context_length] int64 = SOT + ids + EOT,
+ * truncated with the last id forced to EOT, zero padded. */
+int ce_tokenize(ce_tokenizer* t, const char* const* texts, int n, int context_length, int64_t* out);
+/* SimpleTokenizer.decode (tokenizer.py:221-224); *len_out = byte length, buf NUL-terminated. */
+int ce_tokenizer_decode(const ce_tokenizer* t, const int32_t* ids, int n, char* buf, int cap, int* len_out);
 
 #ifdef __cplusplus
 }
