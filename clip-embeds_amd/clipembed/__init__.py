@@ -6,6 +6,7 @@ all compute runs in libclipembed.so (hand-written HIP kernels) behind a C ABI.
 from ._lib import ClipEmbedError, LIB_PATH, exported_symbols
 from .config import ModelConfig, get_model_config, list_models
 from .model import CLIP, Engine, create_model, create_model_and_transforms, load_checkpoint_file
+from .train import TextTowerTrainer
 from .tokenizer import SimpleTokenizer, decode, get_tokenizer, tokenize
 from .transforms import image_transform, prepare_data
 from .weights import (synthetic_captions, synthetic_images, synthetic_images_u8, synthetic_pacl_heads,
@@ -18,4 +19,5 @@ __all__ = [
     "create_model_and_transforms", "exported_symbols", "get_model_config", "image_transform", "list_models",
     "load_checkpoint_file", "prepare_data", "synthetic_captions", "synthetic_images", "synthetic_images_u8",
     "synthetic_pacl_heads", "synthetic_state_dict", "SimpleTokenizer", "tokenize", "decode", "get_tokenizer",
+    "TextTowerTrainer",
 ]

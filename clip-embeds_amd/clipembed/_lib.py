@@ -94,6 +94,14 @@ _SIGNATURES = {
     "ce_set_gemm_splitk": (c_int, [c_int]),
     "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
     "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
+    "ce_train_bind": (c_int, [c_void_p, POINTER(Tensor), POINTER(Tensor), c_int]),
+    "ce_train_sync_weights": (c_int, [c_void_p, c_void_p]),
+    "ce_text_forward_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "ce_text_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    "ce_contrastive_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p,
+                                    c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "ce_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
+                         c_float, c_float, c_int]),
     "ce_tokenizer_create": (c_int, [c_char_p, ctypes.c_size_t, POINTER(c_char_p), c_int, POINTER(c_void_p)]),
     "ce_tokenizer_destroy": (c_int, [c_void_p]),
     "ce_tokenizer_last_error": (c_char_p, []),

@@ -1,0 +1,221 @@
+"""Contrastive training step of the text tower with a locked image tower.
+
+Mirrors one iteration of open_clip_train/train.py:85-189 as launched by
+open_clip/src/train-clip.sh (`--lock-image --local-loss --gather-with-grad [--usehardtext]
+--lr 5e-6 --wd 0.0`, ViT AdamW betas (0.9, 0.98), eps 1e-6, params.py:9), with one process per GPU:
+
+  1. image features: the frozen image tower forward (main.py:271-275 lock_image_tower), normalised;
+  2. text features: the text tower forward with saved activations (ce_text_forward_train);
+  3. ClipLoss (loss.py:137-193): RCCL all-gather of image features, of text sizes + padded text
+     features (gather_features_diffsize :67-87), reorder originals before hard negatives
+     (:144-153), local-loss logits [B, sum T] and [T_local, W*B], labels arange + B*rank with -100
+     for hard negatives (:127-135), loss = (CE_i + CE_t) / 2;
+  4. backward of the loss to the features (ce_contrastive_grad); the all-gather's backward (sum of
+     every rank's gradient of this rank's rows) is an RCCL all_reduce of d(all text features);
+  5. text-tower backward into one flat f32 gradient buffer (ce_text_backward), DDP's gradient
+     all-reduce as ONE RCCL all_reduce(AVG) of that buffer (main.py:302);
+  6. AdamW on the flat f32 masters, two groups as main.py:335-349 (gain/bias/ln/logit_scale
+     without weight decay), then the engine's compute copies are refreshed from the masters
+     (ce_train_sync_weights) and logit_scale is clamped to [0, ln 100] (train.py:189).
+
+All arithmetic is in libclipembed; torch.distributed moves the bytes (RCCL over xGMI, or gloo in
+the CPU tests).  Mixed precision is the engine's (bf16 GEMM operands, f32 accumulation, f32
+masters/gradients), standing in for the reference's `--precision amp`.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .model import CLIP, _ptr, _stream
+
+
+def _excluded(name: str, t: torch.Tensor) -> bool:
+    """main.py:335: no weight decay for 1-d tensors, norms, biases and logit_scale."""
+    return t.ndim < 2 or "bn" in name or "ln" in name or "bias" in name or "logit_scale" in name
+
+
+def text_tensor_names(model: CLIP) -> List[str]:
+    names = ["token_embedding.weight", "positional_embedding", "ln_final.weight", "ln_final.bias", "text_projection"]
+    for l in range(model.cfg.text.layers):
+        for n in ("ln_1.weight", "ln_1.bias", "attn.in_proj_weight", "attn.in_proj_bias", "attn.out_proj.weight",
+                  "attn.out_proj.bias", "ln_2.weight", "ln_2.bias", "mlp.c_fc.weight", "mlp.c_fc.bias",
+                  "mlp.c_proj.weight", "mlp.c_proj.bias"):
+            names.append(f"transformer.resblocks.{l}.{n}")
+    return names
+
+
+def _tensor_entry(name: bytes, t: torch.Tensor) -> _lib.Tensor:
+    e = _lib.Tensor()
+    e.name = name
+    e.data = ctypes.c_void_p(t.data_ptr())
+    e.dtype = _lib.CE_F32
+    e.ndim = t.dim()
+    for d in range(t.dim()):
+        e.shape[d] = t.shape[d]
+    return e
+
+
+def negclip_feature_grad(img: torch.Tensor, txt: torch.Tensor, scale: float, rank: int, world: int, cgrad):
+    """ClipLoss(local_loss=True, gather_with_grad=True, usehardtext=T > B) forward and backward to
+    this rank's text features (loss.py:67-87, 127-193).  img [B, E], txt [B + K, E] (originals
+    first, then this rank's hard negatives; K may differ per rank), both L2-normalised.
+    cgrad(a, b, scale, labels, inv_count, da, db, weight) accumulates one CE direction (the
+    engine's ce_contrastive_grad; a torch double in the CPU tests).  Returns d loss / d txt."""
+    B, T = img.shape[0], txt.shape[0]
+    dev = txt.device
+    dtxt = torch.zeros_like(txt)
+    if world > 1:
+        parts = [torch.empty_like(img) for _ in range(world)]
+        dist.all_gather(parts, img.contiguous())
+        all_img = torch.cat(parts)
+        size = torch.tensor([T], device=dev, dtype=torch.int64)
+        sizes = [torch.empty_like(size) for _ in range(world)]
+        dist.all_gather(sizes, size)
+        sizes = [int(x) for x in sizes]
+        padded = torch.zeros(max(sizes), txt.shape[1], device=dev, dtype=txt.dtype)
+        padded[:T] = txt
+        tparts = [torch.empty_like(padded) for _ in range(world)]
+        dist.all_gather(tparts, padded)
+        # originals of every rank, then hard negatives of every rank (loss.py:144-153)
+        all_txt = torch.cat([p[:B] for p in tparts] + [p[B:n] for p, n in zip(tparts, sizes)]).contiguous()
+        off_h = world * B + sum(n - B for n in sizes[:rank])
+    else:
+        all_img, all_txt = img, txt
+    li = torch.arange(B, device=dev, dtype=torch.long) + (B * rank if world > 1 else 0)
+    lt = torch.cat([li, torch.full((T - B,), -100, device=dev, dtype=torch.long)]) if T > B else li
+    d_all_txt = torch.zeros_like(all_txt)
+    cgrad(img, all_txt, scale, li, 1.0 / B, None, d_all_txt, 0.5)    # CE(logits_per_image, li)
+    cgrad(txt, all_img, scale, lt, 1.0 / B, dtxt, None, 0.5)         # CE(logits_per_text, lt)
+    if world > 1:
+        dist.all_reduce(d_all_txt)                 # backward of the all-gather: sum over ranks
+        dtxt[:B] += d_all_txt[rank * B:(rank + 1) * B]
+        if T > B:
+            dtxt[B:] += d_all_txt[off_h:off_h + T - B]
+    else:
+        dtxt += d_all_txt
+    return dtxt
+
+
+class TextTowerTrainer:
+    """Owns the f32 masters, gradients and AdamW state of the text tower (+ logit_scale) on the
+    model's device, laid out as [decay group | no-decay group | logit_scale] in flat buffers."""
+
+    def __init__(self, model: CLIP, lr: float = 5e-6, betas=(0.9, 0.98), eps: float = 1e-6,
+                 weight_decay: float = 0.0, local_loss: bool = True, gather_with_grad: bool = True,
+                 usehardtext: bool = False, rank: int = 0, world_size: int = 1):
+        if world_size > 1 and not (local_loss and gather_with_grad):
+            raise NotImplementedError("the engine implements the train-clip.sh setting: --local-loss --gather-with-grad")
+        self.model = model
+        self.e = model.engine
+        self.dev = self.e.device
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.usehardtext = usehardtext
+        self.rank, self.world = rank, world_size
+        names = text_tensor_names(model)
+        missing = [n for n in names if n not in model._sd]
+        if missing:
+            raise RuntimeError(f"text tower weights missing from the model's state dict: {missing[:3]}")
+        decay = [n for n in names if not _excluded(n, model._sd[n])]
+        nodecay = [n for n in names if _excluded(n, model._sd[n])]
+        order = decay + nodecay
+        sizes = [model._sd[n].numel() for n in order]
+        self.n_decay = sum(sizes[: len(decay)])
+        self.n_total = sum(sizes) + 1                       # + logit_scale (no-decay group, last)
+        self.param = torch.empty(self.n_total, device=self.dev, dtype=torch.float32)
+        self.grad = torch.zeros_like(self.param)
+        self.exp_avg = torch.zeros_like(self.param)
+        self.exp_avg_sq = torch.zeros_like(self.param)
+        self.views: Dict[str, torch.Tensor] = {}
+        self.gviews: Dict[str, torch.Tensor] = {}
+        off = 0
+        for n, sz in zip(order, sizes):
+            shape = tuple(model._sd[n].shape)
+            self.param[off:off + sz].copy_(model._sd[n].float().reshape(-1).to(self.dev))
+            self.views[n] = self.param[off:off + sz].view(shape)
+            self.gviews[n] = self.grad[off:off + sz].view(shape)
+            off += sz
+        self.param[off] = float(model.logit_scale.detach())
+        self.step_count = 0
+        self._keep = []
+        P = (_lib.Tensor * len(order))()
+        G = (_lib.Tensor * len(order))()
+        for i, n in enumerate(order):
+            b = n.encode()
+            self._keep.append(b)
+            P[i] = _tensor_entry(b, self.views[n])
+            G[i] = _tensor_entry(b, self.gviews[n])
+        _lib.call("ce_train_bind", self.e.h, P, G, len(order))
+        _lib.call("ce_train_sync_weights", self.e.h, _stream(self.dev))
+        self.lossbuf = torch.zeros(2, device=self.dev, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ pieces
+    @property
+    def logit_scale(self) -> torch.Tensor:
+        return self.param[-1]
+
+    def text_forward(self, texts: torch.Tensor) -> torch.Tensor:
+        texts = texts.to(self.dev, torch.int64).contiguous()
+        f = torch.empty(texts.shape[0], self.model.cfg.embed_dim, device=self.dev, dtype=torch.float32)
+        _lib.call("ce_text_forward_train", self.e.h, _stream(self.dev), _ptr(texts), texts.shape[0], _ptr(f))
+        return f
+
+    def _cgrad(self, a, b, scale, labels, inv_count, da, db, weight):
+        _lib.call("ce_contrastive_grad", self.e.h, _stream(self.dev), _ptr(a), a.shape[0], _ptr(b), b.shape[0],
+                  a.shape[1], float(scale), _ptr(labels), float(weight), float(inv_count), _ptr(self.lossbuf),
+                  _ptr(da), _ptr(db))
+
+    def loss_and_feature_grad(self, img: torch.Tensor, txt: torch.Tensor, scale: float):
+        """ClipLoss forward + backward to the local text features (loss.py:137-193)."""
+        self.lossbuf.zero_()
+        return negclip_feature_grad(img, txt, scale, self.rank, self.world, self._cgrad)
+
+    # ------------------------------------------------------------------ the step
+    def compute_grads(self, images: torch.Tensor, texts: torch.Tensor) -> torch.Tensor:
+        """Steps 1-5: forward, ClipLoss, backward, gradient all-reduce.  Returns the local loss (device
+        scalar, no host sync); gradients are in self.grad / self.gviews."""
+        img = self.model.encode_image(images, normalize=True)
+        txt = self.text_forward(texts)
+        scale = math.exp(float(self.logit_scale))
+        dtxt = self.loss_and_feature_grad(img, txt, scale)
+        _lib.call("ce_text_backward", self.e.h, _stream(self.dev), _ptr(dtxt), txt.shape[0])
+        self.grad[-1:].copy_(self.lossbuf[1:2])       # d loss / d logit_scale
+        if self.world > 1:                            # DDP: average over ranks, one flat buffer
+            dist.all_reduce(self.grad)
+            self.grad.div_(self.world)
+        return self.lossbuf[0].clone()
+
+    def apply_update(self, lr: Optional[float] = None):
+        """Step 6: AdamW on both groups, logit_scale clamp, engine weights refreshed."""
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        b1, b2 = self.betas
+        s = _stream(self.dev)
+        _lib.call("ce_adamw", s, _ptr(self.param), _ptr(self.grad), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
+                  self.n_decay, lr, b1, b2, self.eps, self.wd, self.step_count)
+        rest = self.n_total - self.n_decay
+        off = self.n_decay * 4
+        _lib.call("ce_adamw", s, ctypes.c_void_p(self.param.data_ptr() + off),
+                  ctypes.c_void_p(self.grad.data_ptr() + off), ctypes.c_void_p(self.exp_avg.data_ptr() + off),
+                  ctypes.c_void_p(self.exp_avg_sq.data_ptr() + off), rest, lr, b1, b2, self.eps, 0.0, self.step_count)
+        self.param[-1:].clamp_(0, math.log(100))      # train.py:189
+        _lib.call("ce_train_sync_weights", self.e.h, s)
+        with torch.no_grad():
+            self.model.logit_scale.copy_(self.param[-1])
+
+    def step(self, images: torch.Tensor, texts: torch.Tensor, lr: Optional[float] = None) -> float:
+        """One optimizer step on (images [B,3,H,W], texts [B+K,77]); returns the local loss."""
+        loss = self.compute_grads(images, texts)
+        self.apply_update(lr)
+        return float(loss)
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """The text tower's current f32 masters (+ logit_scale), open_clip names."""
+        out = {n: v.detach().cpu().clone() for n, v in self.views.items()}
+        out["logit_scale"] = self.param[-1].detach().cpu().clone()
+        return out

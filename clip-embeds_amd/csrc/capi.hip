@@ -153,6 +153,12 @@ struct ce_handle {
     bool timing = false;
     std::string timing_only;     // non-empty: only launches with this tag are bracketed
     float* cur_part = nullptr;   // GEMM split-K slabs of the tower whose launches are being issued
+    // text-tower training: caller-owned f32 master values and gradient slots per
+    // trainable tensor (device pointers), saved activations of the last ce_text_forward_train
+    std::map<std::string, std::pair<float*, float*>> bound;
+    char* tr = nullptr;
+    size_t tr_bytes = 0;
+    int tr_B = 0;                // batch of the saved activations (0 = none)
     std::vector<KStat> stats;
     std::map<std::string, int> stat_idx;
     std::vector<Pending> pending;
@@ -558,6 +564,229 @@ bool valid_tower(const ce_tower_config& t) {
            t.width % 256 == 0 && t.width <= 1536 && t.mlp_width % 64 == 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Text-tower training: activations saved by the forward, scratch of the backward.  Per layer l:
+// X[l] (block input, f32), XM[l] (after attention, f32), xn1/att/xn2 (bf16 [M][D]), qkv (bf16
+// [M][3D]), pre/hh (c_fc pre-activation and activation, bf16 [M][F]); X[layers] feeds ln_final.
+struct TrainWs {
+    int B = 0, M = 0, Mp = 0, D = 0, F = 0, E = 0, nl = 0;
+    std::vector<float*> X, XM;
+    std::vector<bf16_t*> xn1, qkv, att, xn2, pre, hh;
+    int64_t* ids;
+    int* rows;
+    float *pooled, *u, *f;
+    // backward scratch
+    float *dres, *dxn, *dpool, *du, *pooledT, *colsum, *lnscr;
+    bf16_t *dres_b, *dA, *dB, *TA, *TB, *WT;
+    float* part;
+    void* emb;
+    size_t emb_bytes;
+};
+
+size_t train_layout(const ce_handle* h, int B, TrainWs* w, char* base) {
+    const ce_config& c = h->cfg;
+    const int D = c.text.width, F = c.text.mlp_width, E = c.embed_dim, L = c.context_length, nl = c.text.layers;
+    const long M = (long)B * L, Mp = (M + 63) / 64 * 64;
+    const long NX = std::max(3L * D, (long)F);
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* r = base ? base + off : nullptr;
+        off += align256(bytes);
+        return r;
+    };
+    TrainWs t;
+    t.B = B; t.M = (int)M; t.Mp = (int)Mp; t.D = D; t.F = F; t.E = E; t.nl = nl;
+    for (int l = 0; l <= nl; ++l) t.X.push_back((float*)take(M * D * 4));
+    for (int l = 0; l < nl; ++l) {
+        t.XM.push_back((float*)take(M * D * 4));
+        t.xn1.push_back((bf16_t*)take(M * D * 2));
+        t.qkv.push_back((bf16_t*)take(M * 3 * D * 2));
+        t.att.push_back((bf16_t*)take(M * D * 2));
+        t.xn2.push_back((bf16_t*)take(M * D * 2));
+        t.pre.push_back((bf16_t*)take(M * F * 2));
+        t.hh.push_back((bf16_t*)take(M * F * 2));
+    }
+    t.ids = (int64_t*)take(M * 8);
+    t.rows = (int*)take(B * 4);
+    t.pooled = (float*)take((size_t)B * D * 4);
+    t.u = (float*)take((size_t)B * E * 4);
+    t.f = (float*)take((size_t)B * E * 4);
+    t.dres = (float*)take(M * D * 4);
+    t.dxn = (float*)take(M * D * 4);
+    t.dpool = (float*)take((size_t)B * D * 4);
+    t.du = (float*)take((size_t)B * E * 4);
+    t.pooledT = (float*)take((size_t)B * D * 4);
+    t.colsum = (float*)take(ce::colsum_scratch_floats((int)M, (int)NX) * 4);
+    t.lnscr = (float*)take(ce::ln_bwd_scratch_floats((int)M, D) * 4);
+    t.dres_b = (bf16_t*)take(M * D * 2);
+    t.dA = (bf16_t*)take(M * NX * 2);
+    t.dB = (bf16_t*)take(M * NX * 2);
+    t.TA = (bf16_t*)take(NX * Mp * 2);
+    t.TB = (bf16_t*)take(NX * Mp * 2);
+    t.WT = (bf16_t*)take(NX * D * 2);
+    t.part = (float*)take(ce::kGemmPartElems * 4);
+    t.emb_bytes = ce::embed_bwd_scratch_bytes((int)M);
+    t.emb = take(t.emb_bytes);
+    if (w) *w = t;
+    return off;
+}
+
+int train_ws(ce_handle* h, int B, TrainWs& w) {
+    const size_t need = train_layout(h, B, nullptr, nullptr);
+    CE_TRY(grow_buffer(h->tr, h->tr_bytes, need));
+    train_layout(h, B, &w, h->tr);
+    return CE_OK;
+}
+
+const char* kTextTrainable[] = {"ln_1.weight", "ln_1.bias", "attn.in_proj_weight", "attn.in_proj_bias",
+                                "attn.out_proj.weight", "attn.out_proj.bias", "ln_2.weight", "ln_2.bias",
+                                "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight", "mlp.c_proj.bias"};
+
+std::vector<std::string> text_trainable_names(const ce_handle* h) {
+    std::vector<std::string> v = {"token_embedding.weight", "positional_embedding", "ln_final.weight",
+                                  "ln_final.bias", "text_projection"};
+    for (int l = 0; l < h->cfg.text.layers; ++l)
+        for (const char* n : kTextTrainable) v.push_back("transformer.resblocks." + std::to_string(l) + "." + n);
+    return v;
+}
+
+size_t spec_elems(const ce_handle* h, const std::string& n) {
+    size_t c = 1;
+    for (auto v : h->specs.at(n).shape) c *= (size_t)v;
+    return c;
+}
+
+float* grad_of(ce_handle* h, const std::string& n) { return h->bound.at(n).second; }
+
+int tgemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt, long ldw, int M,
+          int N, int K, const float* bias, int act, const float* resid, void* out, bool out_bf16, float* part) {
+    ce::GemmParams p{};
+    p.A = A; p.lda = lda; p.W = Wt; p.ldw = ldw;
+    p.M = M; p.N = N; p.K = K;
+    p.bias = bias;
+    p.resid = resid; p.ldr = N;
+    p.out = out; p.ldo = N;
+    p.part = part;
+    p.part_elems = part ? ce::kGemmPartElems : 0;
+    return timed(h, s, tag, 2.0 * M * N * K, 0.0, [&] { return ce::launch_gemm(p, act, out_bf16, s); });
+}
+
+// text forward keeping every activation the backward needs (open_clip encode_text, model.py:283-301)
+int run_text_train(ce_handle* h, hipStream_t s, TrainWs& w, const int64_t* ids) {
+    const ce_config& c = h->cfg;
+    const int D = w.D, F = w.F, L = c.context_length, H = c.text.heads, M = w.M, B = w.B;
+    HIP_TRY(hipMemcpyAsync(w.ids, ids, (size_t)M * 8, hipMemcpyDeviceToDevice, s));
+    CE_TRY(check_launch(ce::launch_text_embed(w.X[0], w.ids, W(h, "token_embedding.weight"), W(h, "positional_embedding"),
+                                              B, L, D, c.vocab_size, s), "token_embedding"));
+    for (int l = 0; l < w.nl; ++l) {
+        const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(l) + ".");
+        CE_TRY(layernorm(h, s, "ln_t", w.X[l], w.xn1[l], true, k.ln1w, k.ln1b, M, D));
+        CE_TRY(tgemm(h, s, "train_qkv", w.xn1[l], D, k.wqkv, D, M, 3 * D, D, k.bqkv, ce::ACT_NONE_, nullptr, w.qkv[l],
+                     true, w.part));
+        CE_TRY(timed(h, s, "train_attn", 4.0 * B * H * (double)L * L * 64, 0.0,
+                     [&] { return ce::launch_attention(w.qkv[l], w.att[l], B, L, H, true, true, s); }));
+        CE_TRY(tgemm(h, s, "train_out", w.att[l], D, k.wout, D, M, D, D, k.bout, ce::ACT_NONE_, w.X[l], w.XM[l], false,
+                     w.part));
+        CE_TRY(layernorm(h, s, "ln_t", w.XM[l], w.xn2[l], true, k.ln2w, k.ln2b, M, D));
+        CE_TRY(tgemm(h, s, "train_fc", w.xn2[l], D, k.wfc, D, M, F, D, k.bfc, ce::ACT_NONE_, nullptr, w.pre[l], true,
+                     w.part));
+        CE_TRY(check_launch(ce::launch_act(w.hh[l], w.pre[l], nullptr, (long)M * F, act_code(h), s), "act"));
+        CE_TRY(tgemm(h, s, "train_proj", w.hh[l], F, k.wproj, F, M, D, F, k.bproj, ce::ACT_NONE_, w.XM[l], w.X[l + 1],
+                     false, w.part));
+    }
+    CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, w.ids, B, L, s), "argmax"));
+    CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.X[w.nl], w.rows, D, B, D, W(h, "ln_final.weight"),
+                                             W(h, "ln_final.bias"), s), "ln_final(pool)"));
+    ce::FGemmParams fp{};
+    fp.A = w.pooled; fp.lda = D; fp.B = W(h, "text_projection"); fp.ldb = w.E;
+    fp.C = w.u; fp.ldc = w.E; fp.M = B; fp.N = w.E; fp.K = D; fp.batch = 1; fp.alpha = 1.f;
+    CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "text_projection"));
+    CE_TRY(check_launch(ce::launch_l2norm(w.f, w.u, B, w.E, s), "normalize"));
+    return CE_OK;
+}
+
+// d(loss)/d(every bound text tensor) from d(loss)/d(normalised features) [B][E]
+int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfeat) {
+    const ce_config& c = h->cfg;
+    const int D = w.D, F = w.F, E = w.E, L = c.context_length, H = c.text.heads, M = w.M, Mp = w.Mp, B = w.B;
+    const int act = act_code(h);
+    // F.normalize, projection, ln_final on the EOT rows (transformer.py:839-855, model.py:300)
+    CE_TRY(check_launch(ce::launch_l2norm_bwd(w.du, w.u, dfeat, B, E, s), "l2norm_bwd"));
+    CE_TRY(check_launch(ce::launch_transpose_f32(w.pooledT, B, w.pooled, D, B, D, s), "transpose"));
+    {
+        ce::FGemmParams fp{};      // d text_projection [D][E] = pooled^T du
+        fp.A = w.pooledT; fp.lda = B; fp.B = w.du; fp.ldb = E; fp.C = grad_of(h, "text_projection"); fp.ldc = E;
+        fp.M = D; fp.N = E; fp.K = B; fp.batch = 1; fp.alpha = 1.f;
+        CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "d_text_projection"));
+        ce::FGemmParams fq{};      // d pooled [B][D] = du proj^T
+        fq.A = w.du; fq.lda = E; fq.B = W(h, "text_projection"); fq.ldb = E; fq.C = w.dpool; fq.ldc = D;
+        fq.M = B; fq.N = D; fq.K = E; fq.batch = 1; fq.alpha = 1.f;
+        CE_TRY(check_launch(ce::launch_fgemm(fq, true, s), "d_pooled"));
+    }
+    HIP_TRY(hipMemsetAsync(w.dres, 0, (size_t)M * D * 4, s));
+    CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.X[w.nl], w.dpool, D, W(h, "ln_final.weight"), w.rows, B, D,
+                                          grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
+                                          w.lnscr, s), "ln_final_bwd"));
+    const float qs = ce::kAttnQScale;
+    for (int l = w.nl - 1; l >= 0; --l) {
+        const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
+        const Blk k = block_ptrs(h, pfx);
+        auto G = [&](const char* n) { return grad_of(h, pfx + n); };
+        // ---- MLP: X[l+1] = XM + c_proj(act(c_fc(ln_2 XM)))  (transformer.py:235-239, 267) ----
+        CE_TRY(check_launch(ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s), "cast"));
+        CE_TRY(check_launch(ce::launch_colsum(G("mlp.c_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s),
+                            "colsum"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s), "transpose"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dW_proj", w.TA, Mp, w.TB, Mp, D, F, Mp, nullptr, 0, nullptr, G("mlp.c_proj.weight"), false,
+                     w.part));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
+        CE_TRY(check_launch(ce::launch_act(w.dA, w.pre[l], w.dA, (long)M * F, act, s), "act_bwd"));
+        CE_TRY(check_launch(ce::launch_colsum(G("mlp.c_fc.bias"), w.dA, false, F, M, F, 1.f, false, w.colsum, s),
+                            "colsum"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s), "transpose"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dW_fc", w.TA, Mp, w.TB, Mp, F, D, Mp, nullptr, 0, nullptr, G("mlp.c_fc.weight"), false,
+                     w.part));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, w.dxn, false, w.part));
+        CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
+                                              G("ln_2.bias"), true, false, w.lnscr, s), "ln_2_bwd"));
+        // ---- attention: XM = X + out_proj(MHA(ln_1 X))  (transformer.py:242-255, 266) ----
+        CE_TRY(check_launch(ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s), "cast"));
+        CE_TRY(check_launch(ce::launch_colsum(G("attn.out_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s),
+                            "colsum"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s), "transpose"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dW_out", w.TA, Mp, w.TB, Mp, D, D, Mp, nullptr, 0, nullptr, G("attn.out_proj.weight"),
+                     false, w.part));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, D, k.wout, false, D, D, D, D, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dX_out", w.dres_b, D, w.WT, D, M, D, D, nullptr, 0, nullptr, w.dB, true, w.part));
+        CE_TRY(timed(h, s, "attn_bwd", 10.0 * B * H * (double)L * L * 64, 0.0, [&] {
+            return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, B, L, H, true, s);
+        }));
+        // in_proj: the engine's q rows carry kAttnQScale, so d(master q rows) = qs * d(engine q rows)
+        CE_TRY(check_launch(ce::launch_colsum(G("attn.in_proj_bias"), w.dA, false, 3 * D, M, 3 * D, 1.f, false,
+                                              w.colsum, s), "colsum"));
+        CE_TRY(check_launch(ce::launch_scale(G("attn.in_proj_bias"), D, qs, s), "scale"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s), "transpose"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(tgemm(h, s, "dW_qkv", w.TA, Mp, w.TB, Mp, 3 * D, D, Mp, nullptr, 0, nullptr, G("attn.in_proj_weight"),
+                     false, w.part));
+        CE_TRY(check_launch(ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s), "scale"));
+        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s),
+                            "transpose"));
+        CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, w.dxn, false, w.part));
+        CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.X[l], w.dxn, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
+                                              G("ln_1.bias"), true, false, w.lnscr, s), "ln_1_bwd"));
+    }
+    // token / positional embeddings (model.py:286-288)
+    CE_TRY(check_launch(ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),
+                                             w.dres, w.ids, B, L, D, c.vocab_size, w.emb, w.emb_bytes, s), "embed_bwd"));
+    return CE_OK;
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -625,6 +854,7 @@ int ce_destroy(ce_handle* h) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->ws_t) (void)hipFree(h->ws_t);
     if (h->tmp) (void)hipFree(h->tmp);
+    if (h->tr) (void)hipFree(h->tr);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->prep_host) (void)hipHostFree(h->prep_host);
     if (h->prep_dev) (void)hipFree(h->prep_dev);
@@ -1344,6 +1574,134 @@ int ce_kernel_layernorm(void* stream, const float* in, void* out, int out_dtype,
     ce::LNParams p{};
     p.in = in; p.ldi = D; p.out = out; p.ldo = D; p.w = w; p.b = b; p.rows = rows; p.D = D;
     return check_launch(ce::launch_layernorm(p, out_dtype == CE_BF16, (hipStream_t)stream), "layernorm");
+}
+
+// ---- text-tower training -------------------------------------------------
+int ce_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* grads, int n) {
+    if (!h || (n > 0 && (!params || !grads))) return fail(CE_ERR_INVALID, "ce_train_bind: null argument");
+    std::map<std::string, std::pair<float*, float*>> b;
+    for (int i = 0; i < n; ++i) {
+        if (!params[i].name || !grads[i].name || strcmp(params[i].name, grads[i].name) != 0)
+            return fail(CE_ERR_INVALID, "ce_train_bind: entry %d: params and grads must name the same tensor", i);
+        const std::string name = canonical(h, params[i].name);
+        auto it = h->specs.find(name);
+        if (it == h->specs.end()) return fail(CE_ERR_INVALID, "ce_train_bind: unknown tensor '%s'", params[i].name);
+        if (params[i].dtype != CE_F32 || grads[i].dtype != CE_F32 || !params[i].data || !grads[i].data)
+            return fail(CE_ERR_INVALID, "ce_train_bind: '%s' needs f32 device buffers", params[i].name);
+        for (const ce_tensor* t : {&params[i], &grads[i]}) {
+            bool ok = t->ndim == (int)it->second.shape.size();
+            for (int d = 0; ok && d < t->ndim; ++d) ok = t->shape[d] == it->second.shape[d];
+            if (!ok) return fail(CE_ERR_INVALID, "ce_train_bind: '%s' has the wrong shape", params[i].name);
+        }
+        b[name] = {(float*)params[i].data, (float*)grads[i].data};
+    }
+    for (const std::string& nm : text_trainable_names(h))
+        if (!b.count(nm)) return fail(CE_ERR_INVALID, "ce_train_bind: text tensor '%s' not bound", nm.c_str());
+    h->bound = b;
+    return CE_OK;
+}
+
+int ce_train_sync_weights(ce_handle* h, void* stream) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_train_sync_weights: null handle");
+    if (h->bound.empty()) return fail(CE_ERR_STATE, "ce_train_sync_weights: no tensors bound (ce_train_bind)");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    for (auto& kv : h->bound) {
+        const WSpec& sp = h->specs.at(kv.first);
+        const size_t n = spec_elems(h, kv.first);
+        void*& dp = h->dptr[kv.first];
+        if (!dp) {
+            const size_t bytes = n * (sp.st == ST_BF16 ? 2 : 4);
+            if (hipMalloc(&dp, bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                h->dptr.erase(kv.first);
+                return fail(CE_ERR_OOM, "ce_train_sync_weights: cannot allocate '%s'", kv.first.c_str());
+            }
+        }
+        const bool inproj = kv.first.size() > 12 && kv.first.find("attn.in_proj_") != std::string::npos;
+        const long row = sp.shape.size() == 2 ? sp.shape[1] : 1;
+        const long qrows = inproj ? sp.shape[0] / 3 : 0;
+        if (sp.st != ST_BF16 && sp.st != ST_F32)
+            return fail(CE_ERR_INVALID, "ce_train_sync_weights: '%s' has an unsupported storage", kv.first.c_str());
+        CE_TRY(check_launch(ce::launch_weight_from_master(dp, sp.st == ST_BF16, kv.second.first, (long)n, row, qrows,
+                                                          ce::kAttnQScale, s), "weight_from_master"));
+        h->loaded[kv.first] = true;
+    }
+    return CE_OK;
+}
+
+int ce_text_forward_train(ce_handle* h, void* stream, const int64_t* ids, int B, float* out_features) {
+    if (!h || !ids) return fail(CE_ERR_INVALID, "ce_text_forward_train: null argument");
+    if (B <= 0) return fail(CE_ERR_INVALID, "ce_text_forward_train: batch must be positive");
+    if (h->cfg.context_length > 80)
+        return fail(CE_ERR_INVALID, "ce_text_forward_train: context %d > 80 (attention backward)", h->cfg.context_length);
+    CE_TRY(check_ready(h, false));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    TrainWs w;
+    CE_TRY(train_ws(h, B, w));
+    CE_TRY(run_text_train(h, s, w, ids));
+    h->tr_B = B;
+    if (out_features)
+        HIP_TRY(hipMemcpyAsync(out_features, w.f, (size_t)B * w.E * 4, hipMemcpyDeviceToDevice, s));
+    return CE_OK;
+}
+
+int ce_text_backward(ce_handle* h, void* stream, const float* d_features, int B) {
+    if (!h || !d_features) return fail(CE_ERR_INVALID, "ce_text_backward: null argument");
+    if (h->bound.empty()) return fail(CE_ERR_STATE, "ce_text_backward: no gradient buffers bound (ce_train_bind)");
+    if (B != h->tr_B || B <= 0)
+        return fail(CE_ERR_STATE, "ce_text_backward: batch %d does not match the last ce_text_forward_train (%d)", B,
+                    h->tr_B);
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    TrainWs w;
+    train_layout(h, B, &w, h->tr);
+    return run_text_backward(h, s, w, d_features);
+}
+
+int ce_contrastive_grad(ce_handle* h, void* stream, const float* A, int Ra, const float* Bm, int Cb, int E, float scale,
+                        const int64_t* labels, float weight, float inv_count, float* out2, float* dA, float* dB) {
+    if (!h || !A || !Bm || !labels || !out2) return fail(CE_ERR_INVALID, "ce_contrastive_grad: null argument");
+    if (Ra <= 0 || Cb <= 0 || E <= 0) return fail(CE_ERR_INVALID, "ce_contrastive_grad: bad sizes");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t zR = (size_t)Ra * Cb;
+    CE_TRY(ensure_tmp(h, (zR * 2 + 2 * (size_t)Ra + (size_t)std::max(Ra, Cb) * E) * 4));
+    float* z = (float*)h->tmp;
+    float* zt = z + zR;
+    float* rowstat = zt + zR;
+    float* acc = rowstat + 2 * (size_t)Ra;
+    ce::FGemmParams fp{};       // z = scale * A B^T (ClipLoss logits, loss.py:155-157)
+    fp.A = A; fp.lda = E; fp.B = Bm; fp.ldb = E; fp.C = z; fp.ldc = Cb;
+    fp.M = Ra; fp.N = Cb; fp.K = E; fp.batch = 1; fp.alpha = scale;
+    CE_TRY(check_launch(ce::launch_fgemm(fp, true, s), "logits"));
+    CE_TRY(check_launch(ce::launch_ce_grad(z, z, Ra, Cb, labels, weight * inv_count, rowstat, out2, s), "ce_grad"));
+    if (dA) {                   // dA += scale * G B
+        ce::FGemmParams q{};
+        q.A = z; q.lda = Cb; q.B = Bm; q.ldb = E; q.C = acc; q.ldc = E;
+        q.M = Ra; q.N = E; q.K = Cb; q.batch = 1; q.alpha = scale;
+        CE_TRY(check_launch(ce::launch_fgemm(q, false, s), "dA"));
+        CE_TRY(check_launch(ce::launch_axpy(dA, acc, (long)Ra * E, 1.f, s), "axpy"));
+    }
+    if (dB) {                   // dB += scale * G^T A
+        CE_TRY(check_launch(ce::launch_transpose_f32(zt, Ra, z, Cb, Ra, Cb, s), "transpose"));
+        ce::FGemmParams q{};
+        q.A = zt; q.lda = Ra; q.B = A; q.ldb = E; q.C = acc; q.ldc = E;
+        q.M = Cb; q.N = E; q.K = Ra; q.batch = 1; q.alpha = scale;
+        CE_TRY(check_launch(ce::launch_fgemm(q, false, s), "dB"));
+        CE_TRY(check_launch(ce::launch_axpy(dB, acc, (long)Cb * E, 1.f, s), "axpy"));
+    }
+    return CE_OK;
+}
+
+int ce_adamw(void* stream, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+             float beta1, float beta2, float eps, float weight_decay, int step) {
+    if (n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)))
+        return fail(CE_ERR_INVALID, "ce_adamw: null argument");
+    if (step < 1) return fail(CE_ERR_INVALID, "ce_adamw: step counts from 1 (got %d)", step);
+    return check_launch(ce::launch_adamw(param, grad, exp_avg, exp_avg_sq, (long)n, lr, beta1, beta2, eps, weight_decay,
+                                         step, (hipStream_t)stream), "adamw");
 }
 
 }  // extern "C"

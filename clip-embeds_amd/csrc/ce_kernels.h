@@ -124,4 +124,41 @@ hipError_t launch_preprocess(const uint8_t* images, const PrepMeta* meta, const 
                              void* tmp, int B, int max_rows, int S, bool pacl, bool out_bf16, const float* mean,
                              const float* stdv, void* out, hipStream_t s);
 
+
+// ---- text-tower training (train.hip) ----
+// out[c][r] (row stride ldo) = in[r][c] for r < R; output columns r in [R, Rpad) are zero.
+hipError_t launch_transpose_bf16(bf16_t* out, long ldo, const void* in, bool in_f32, long ldi, int R, int C, int Rpad,
+                                 hipStream_t s);
+hipError_t launch_transpose_f32(float* out, long ldo, const float* in, long ldi, int R, int C, hipStream_t s);
+// out[n] (+)= scale * sum_m in[m][n]  (deterministic two-stage; scratch >= colsum_scratch_floats)
+long colsum_scratch_floats(int M, int N);
+hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M, int N, float scale, bool accumulate,
+                         float* scratch, hipStream_t s);
+// LayerNorm backward (eps 1e-5): dres[xrow] (+)= dx; dw, db (+)= column sums (scratch >= ln_bwd_scratch_floats)
+long ln_bwd_scratch_floats(int n, int D);
+hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
+                         int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
+                         hipStream_t s);
+// dh == nullptr: out = act(pre); else out = dh * act'(pre).  bf16, n % 8 == 0.
+hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s);
+// attention backward (L <= 80): dqkv [B*L][3*H*64] from qkv (q pre-scaled), O, dO [B*L][H*64]
+hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, int B, int L, int H,
+                                bool causal, hipStream_t s);
+// token / positional embedding gradients from dx [B*ctx][D] (dtok fully overwritten)
+size_t embed_bwd_scratch_bytes(int n);
+hipError_t launch_embed_bwd(float* dtok, float* dpos, const float* dx, const int64_t* ids, int B, int ctx, int D,
+                            int vocab, void* scratch, size_t scratch_bytes, hipStream_t s);
+hipError_t launch_l2norm_bwd(float* du, const float* u, const float* df, int rows, int D, hipStream_t s);
+// CE + gradient over rows of z (labels -100 ignored): g = w/count (softmax - onehot); out2[0] += loss,
+// out2[1] += sum g z.  rowstat: 2R floats.
+hipError_t launch_ce_grad(float* g, const float* z, int R, int C, const int64_t* labels, float wgt_inv_count,
+                          float* rowstat, float* out2, hipStream_t s);
+hipError_t launch_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
+                        float wd, int step, hipStream_t s);
+hipError_t launch_weight_from_master(void* out, bool bf16, const float* src, long n, long row_len, long scale_rows,
+                                     float scale, hipStream_t s);
+hipError_t launch_scale(float* x, long n, float sc, hipStream_t s);
+hipError_t launch_cast_bf16(bf16_t* out, const float* in, long n, hipStream_t s);
+hipError_t launch_axpy(float* y, const float* x, long n, float a, hipStream_t s);   // y += a x
+
 }  // namespace ce

@@ -932,10 +932,19 @@ void plan_tail(GemmParams& p, int nwg) {
     p.tail = 0;
     p.split = 1;
     const int C = num_cus(), nk = p.K / BK;
-    if (!splitk_enabled() || !p.part || nwg <= C) return;
-    const int R = nwg % C;
-    if (R == 0 || R > C / 32) return;     // measured: R = 4 (out/c_proj) gains 3-5 %, R = 12 (QKV) loses
-    int S = std::min(std::min(nk, 16), C / R);
+    if (!splitk_enabled() || !p.part) return;
+    int R, cap;
+    if (nwg <= C / 2 && nk >= 32) {
+        // small grid, long K (weight gradients: M = out features, K = tokens): split every tile
+        R = nwg;
+        cap = 64;
+    } else {
+        if (nwg <= C) return;
+        R = nwg % C;
+        if (R == 0 || R > C / 32) return;     // measured: R = 4 (out/c_proj) gains 3-5 %, R = 12 (QKV) loses
+        cap = 16;
+    }
+    int S = std::min(std::min(nk, cap), C / R);
     while (S >= 2 && (long)R * S * BM * BN > p.part_elems) --S;
     if (S < 2) return;
     p.tail = R;

@@ -1,0 +1,659 @@
+// Text-tower training kernels for gfx950 (the NegCLIP step of
+// open_clip_train/train.py:85-189 with --lock-image, train-clip.sh:22): everything the backward
+// of the text transformer, its pooling/projection/normalisation and the contrastive loss need
+// beyond the forward kernels, plus AdamW.
+//
+// Reference semantics (the autograd of):
+//   ResidualAttentionBlock     open_clip/src/open_clip/transformer.py:257-268 (MHA :242-255, MLP :235-239)
+//   LayerNorm                  transformer.py:23-29 (eps 1e-5)
+//   GELU (erf) / QuickGELU     torch.nn.GELU / transformer.py:32-35
+//   token + positional embed   model.py:286-288;  EOT pooling + projection  transformer.py:839-855
+//   F.normalize                model.py:300
+//   ClipLoss / NegCLIP         open_clip/src/open_clip/loss.py:137-193 (CE, ignore_index -100)
+//   AdamW                      torch.optim.AdamW (open_clip_train/main.py: betas, eps, wd groups)
+#include "ce_device.h"
+#include "ce_kernels.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace ce {
+namespace {
+
+template <typename T> __device__ __forceinline__ float ld_f(const T* p);
+template <> __device__ __forceinline__ float ld_f<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> __device__ __forceinline__ void st_f(T* p, float v);
+template <> __device__ __forceinline__ void st_f<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------------------------------------
+// out[c][r] = in[r][c] for r < R, c < C; rows r in [R, Rpad) of the output are zero (so a GEMM
+// can contract over a K padded to a multiple of 64).  64x64 tiles through LDS.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void transpose_k(TO* __restrict__ out, long ldo, const TI* __restrict__ in,
+                                                   long ldi, int R, int C, int Rpad) {
+    __shared__ float tile[64][65];
+    const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int r = r0 + ty + 4 * k, c = c0 + tx;
+        tile[ty + 4 * k][tx] = (r < R && c < C) ? ld_f(in + (size_t)r * ldi + c) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int c = c0 + ty + 4 * k, r = r0 + tx;
+        if (c < C && r < Rpad) st_f(out + (size_t)c * ldo + r, tile[tx][ty + 4 * k]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Column sums, deterministic two-stage: part[blk][n] = sum of rows blk*CS .. +CS-1, then
+// out[n] = scale * sum_blk part[blk][n] (+ out[n] when accumulate).
+constexpr int CS = 256;
+template <typename TI>
+__global__ __launch_bounds__(256) void colsum_part_k(float* __restrict__ part, const TI* __restrict__ in, long ld,
+                                                     int M, int N) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    const int m0 = blockIdx.y * CS, m1 = min(M, m0 + CS);
+    float s = 0.f;
+    for (int m = m0; m < m1; ++m) s += ld_f(in + (size_t)m * ld + n);
+    part[(size_t)blockIdx.y * N + n] = s;
+}
+__global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, const float* __restrict__ part,
+                                                       int nb, int N, float scale, int accumulate) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += part[(size_t)b * N + n];
+    out[n] = (accumulate ? out[n] : 0.f) + scale * s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm backward, one wave per row (element e = c*256 + lane*4 .. +3, as layernorm_k):
+//   xh = (x - mu) * rstd;  g = dy * w;  dx = rstd * (g - mean(g) - xh * mean(g * xh))
+//   dres[row] (+)= dx;  part_w[blk] += dy * xh;  part_b[blk] += dy
+// rows != null: x and dres rows are rows[i] (EOT pooling), dy row is i.
+constexpr int LNB_ROWS = 64;   // rows per block (partial dw/db per block)
+template <int NC>
+__global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const float* __restrict__ x,
+                                                const float* __restrict__ dy, long ldy, const float* __restrict__ w,
+                                                const int* __restrict__ rows, int n, float* __restrict__ part_w,
+                                                float* __restrict__ part_b, int accumulate) {
+    constexpr int D = NC * 256;
+    __shared__ float red[2][4][D];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float4 aw[NC], ab[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) aw[c] = ab[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int r0 = blockIdx.x * LNB_ROWS;
+    for (int i = r0 + wave; i < min(n, r0 + LNB_ROWS); i += 4) {
+        const long xr = rows ? rows[i] : i;
+        float4 v[NC], g[NC], d[NC];
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int e = c * 256 + lane * 4;
+            v[c] = *reinterpret_cast<const float4*>(x + xr * D + e);
+            d[c] = *reinterpret_cast<const float4*>(dy + (long)i * ldy + e);
+            s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+        }
+        const float mean = wave_sum(s) / (float)D;
+        float q = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            v[c].x -= mean; v[c].y -= mean; v[c].z -= mean; v[c].w -= mean;
+            q += (v[c].x * v[c].x + v[c].y * v[c].y) + (v[c].z * v[c].z + v[c].w * v[c].w);
+        }
+        const float rstd = rsqrtf(wave_sum(q) / (float)D + 1e-5f);
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int e = c * 256 + lane * 4;
+            const float4 ww = *reinterpret_cast<const float4*>(w + e);
+            v[c].x *= rstd; v[c].y *= rstd; v[c].z *= rstd; v[c].w *= rstd;       // xh
+            g[c] = make_float4(d[c].x * ww.x, d[c].y * ww.y, d[c].z * ww.z, d[c].w * ww.w);
+            sg += (g[c].x + g[c].y) + (g[c].z + g[c].w);
+            sgx += (g[c].x * v[c].x + g[c].y * v[c].y) + (g[c].z * v[c].z + g[c].w * v[c].w);
+            aw[c].x += d[c].x * v[c].x; aw[c].y += d[c].y * v[c].y; aw[c].z += d[c].z * v[c].z; aw[c].w += d[c].w * v[c].w;
+            ab[c].x += d[c].x; ab[c].y += d[c].y; ab[c].z += d[c].z; ab[c].w += d[c].w;
+        }
+        const float mg = wave_sum(sg) / (float)D, mgx = wave_sum(sgx) / (float)D;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int e = c * 256 + lane * 4;
+            float4* o = reinterpret_cast<float4*>(dres + xr * D + e);
+            float4 dx = make_float4(rstd * (g[c].x - mg - v[c].x * mgx), rstd * (g[c].y - mg - v[c].y * mgx),
+                                    rstd * (g[c].z - mg - v[c].z * mgx), rstd * (g[c].w - mg - v[c].w * mgx));
+            if (accumulate) {
+                const float4 old = *o;
+                dx.x += old.x; dx.y += old.y; dx.z += old.z; dx.w += old.w;
+            }
+            *o = dx;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int e = c * 256 + lane * 4;
+        *reinterpret_cast<float4*>(&red[0][wave][e]) = aw[c];
+        *reinterpret_cast<float4*>(&red[1][wave][e]) = ab[c];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < D; e += 256) {
+        part_w[(size_t)blockIdx.x * D + e] = (red[0][0][e] + red[0][1][e]) + (red[0][2][e] + red[0][3][e]);
+        part_b[(size_t)blockIdx.x * D + e] = (red[1][0][e] + red[1][1][e]) + (red[1][2][e] + red[1][3][e]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Activation forward (h = act(pre)) and backward (dpre = dh * act'(pre)), bf16, 8 per thread.
+__device__ __forceinline__ float gelu_grad(float x) {      // d/dx [x * Phi(x)] = Phi(x) + x phi(x)
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+__device__ __forceinline__ float qgelu_grad(float x) {
+    const float sg = 1.0f / (1.0f + __expf(-1.702f * x));
+    return sg * (1.0f + 1.702f * x * (1.0f - sg));
+}
+template <int ACT, bool BWD>
+__global__ __launch_bounds__(256) void act_k(bf16_t* __restrict__ out, const bf16_t* __restrict__ pre,
+                                             const bf16_t* __restrict__ dh, long n8) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n8) return;
+    const uint4 pv = reinterpret_cast<const uint4*>(pre)[i];
+    const bf16_t* ps = reinterpret_cast<const bf16_t*>(&pv);
+    uint4 dv;
+    if constexpr (BWD) dv = reinterpret_cast<const uint4*>(dh)[i];
+    const bf16_t* ds = reinterpret_cast<const bf16_t*>(&dv);
+    uint4 ov;
+    bf16_t* os = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float x = bf2f(ps[k]);
+        float y;
+        if constexpr (BWD) y = bf2f(ds[k]) * (ACT == ACT_QGELU ? qgelu_grad(x) : gelu_grad(x));
+        else y = apply_act<ACT>(x);
+        os[k] = f2bf(y);
+    }
+    reinterpret_cast<uint4*>(out)[i] = ov;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Attention backward for one (batch, head) per workgroup, L <= 80 (the text context, 77), d = 64,
+// on MFMA (v_mfma_f32_16x16x32_bf16).  q arrives pre-scaled (q' = q * log2(e)/8: the forward's
+// convention, attention.hip), so S = q' k^T is in log2 units and P = exp2(S - m) / Z.  With
+// delta_i = dO_i . O_i (O = the forward output):
+//   dP = dO V^T;  dS = ln2 * P o (dP - delta);  dq' = dS K;  dk = dS^T q';  dv = P^T dO
+// dq' is the gradient w.r.t. the stored (pre-scaled) q; the in_proj chain rule is applied by the
+// caller.  LDS: row-major q', k, v, dO [80][64]; transposed q'^T, k^T, dO^T [64][96]; P^T, dS, dS^T
+// [80][96] bf16 (contraction dims zero-padded to 96 = 3 x 32); S/P f32 [80][80].
+constexpr int AB_L = 80, AB_KP = 96;
+__device__ __forceinline__ bf16x8 lds_frag(const bf16_t* base, int ld, int row, int k0) {
+    return *reinterpret_cast<const bf16x8*>(base + row * ld + k0);
+}
+// C[16 x 16 tile (ti, tj)] = sum_k X[ti*16 + r][k] * Y[tj*16 + c][k], k < 32 * nk (both K-contiguous).
+// Returns the lane's f32x4: rows ti*16 + 4*(lane>>4) + q (q = 0..3), column tj*16 + (lane&15).
+__device__ __forceinline__ f32x4 mfma_tile(const bf16_t* X, int ldx, const bf16_t* Y, int ldy, int ti, int tj,
+                                           int nk, int lane) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int r = lane & 15, kc = (lane >> 4) * 8;
+    for (int k = 0; k < nk; ++k) {
+        const bf16x8 a = lds_frag(X, ldx, ti * 16 + r, k * 32 + kc);
+        const bf16x8 b = lds_frag(Y, ldy, tj * 16 + r, k * 32 + kc);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ qkv,
+                                                  const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                  int L, int H, int causal) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][64]
+    bf16_t* Ks = Qs + AB_L * 64;
+    bf16_t* Vs = Ks + AB_L * 64;
+    bf16_t* dOs = Vs + AB_L * 64;
+    bf16_t* QT = dOs + AB_L * 64;                            // [64][96]
+    bf16_t* KT = QT + 64 * AB_KP;
+    bf16_t* dOT = KT + 64 * AB_KP;
+    bf16_t* PT = dOT + 64 * AB_KP;                           // [80][96]
+    bf16_t* dS = PT + AB_L * AB_KP;
+    bf16_t* dST = dS + AB_L * AB_KP;
+    float* Sf = reinterpret_cast<float*>(dST + AB_L * AB_KP);  // [80][80]
+    float* delta = Sf + AB_L * AB_L;                          // [80]
+
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int D = H * 64, ld = 3 * D;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // zero the padded operands (rows >= L of the row-major images, columns >= L of the others)
+    for (int e = tid; e < 3 * 64 * AB_KP + 3 * AB_L * AB_KP; e += 256) QT[e] = 0;
+    __syncthreads();
+    // load q', k, v, dO rows (16 B per thread-chunk) + delta_i = dO_i . O_i
+    for (int e = tid; e < AB_L * 8; e += 256) {
+        const int i = e >> 3, c = (e & 7) * 8;
+        uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, g = q, o = q;
+        if (i < L) {
+            const size_t row = (size_t)(b * L + i);
+            q = *reinterpret_cast<const uint4*>(qkv + row * ld + h * 64 + c);
+            k = *reinterpret_cast<const uint4*>(qkv + row * ld + D + h * 64 + c);
+            v = *reinterpret_cast<const uint4*>(qkv + row * ld + 2 * D + h * 64 + c);
+            g = *reinterpret_cast<const uint4*>(dO + row * D + h * 64 + c);
+            o = *reinterpret_cast<const uint4*>(O + row * D + h * 64 + c);
+        }
+        *reinterpret_cast<uint4*>(Qs + i * 64 + c) = q;
+        *reinterpret_cast<uint4*>(Ks + i * 64 + c) = k;
+        *reinterpret_cast<uint4*>(Vs + i * 64 + c) = v;
+        *reinterpret_cast<uint4*>(dOs + i * 64 + c) = g;
+        const bf16_t* qs = reinterpret_cast<const bf16_t*>(&q);
+        const bf16_t* ks = reinterpret_cast<const bf16_t*>(&k);
+        const bf16_t* gs = reinterpret_cast<const bf16_t*>(&g);
+        const bf16_t* os = reinterpret_cast<const bf16_t*>(&o);
+        float part = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            QT[(c + t) * AB_KP + i] = qs[t];
+            KT[(c + t) * AB_KP + i] = ks[t];
+            dOT[(c + t) * AB_KP + i] = gs[t];
+            part += bf2f(gs[t]) * bf2f(os[t]);
+        }
+        // the 8 chunks of row i are 8 consecutive lanes of one wave
+        part += __shfl_xor(part, 1, 64);
+        part += __shfl_xor(part, 2, 64);
+        part += __shfl_xor(part, 4, 64);
+        if ((e & 7) == 0) delta[i] = part;
+    }
+    __syncthreads();
+    const int nt = (L + 15) / 16;
+    // S = q' k^T (f32, log2 units)
+    for (int t = wave; t < nt * nt; t += 4) {
+        const int ti = t / nt, tj = t - ti * nt;
+        const f32x4 s = mfma_tile(Qs, 64, Ks, 64, ti, tj, 2, lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Sf[(ti * 16 + 4 * (lane >> 4) + q) * AB_L + tj * 16 + (lane & 15)] = s[q];
+    }
+    __syncthreads();
+    // row softmax (one wave per row; j < L and, causal, j <= i); P kept f32 in Sf, P^T bf16
+    for (int i = wave; i < L; i += 4) {
+        const int jmax = causal ? i + 1 : L;
+        float m = -INFINITY;
+        for (int j = lane; j < jmax; j += 64) m = fmaxf(m, Sf[i * AB_L + j]);
+        m = wave_max(m);
+        float z = 0.f;
+        for (int j = lane; j < jmax; j += 64) z += exp2f(Sf[i * AB_L + j] - m);
+        z = wave_sum(z);
+        const float iz = 1.0f / z;
+        for (int j = lane; j < AB_L; j += 64) {
+            const float p = j < jmax ? exp2f(Sf[i * AB_L + j] - m) * iz : 0.f;
+            Sf[i * AB_L + j] = p;
+            PT[j * AB_KP + i] = f2bf(p);
+        }
+    }
+    __syncthreads();
+    // dP = dO V^T -> dS = ln2 * P (dP - delta), bf16 both orientations
+    for (int t = wave; t < nt * nt; t += 4) {
+        const int ti = t / nt, tj = t - ti * nt;
+        const f32x4 dp = mfma_tile(dOs, 64, Vs, 64, ti, tj, 2, lane);
+        const int j = tj * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = ti * 16 + 4 * (lane >> 4) + q;
+            const float p = (i < L && j < L) ? Sf[i * AB_L + j] : 0.f;
+            const float ds = 0.69314718055994531f * p * (dp[q] - delta[i < L ? i : 0]);
+            const bf16_t v = f2bf(ds);
+            dS[i * AB_KP + j] = v;
+            dST[j * AB_KP + i] = v;
+        }
+    }
+    __syncthreads();
+    // dq' = dS K (contract j: X = dS [i][j], Y = K^T [d][j]); dk = dS^T q' (X = dS^T, Y = q'^T);
+    // dv = P^T dO (X = P^T [j][i], Y = dO^T [d][i]).  16 x 16 output tiles: nt x 4 per product.
+    const int nkk = (L + 31) / 32;
+    for (int t = wave; t < 3 * nt * 4; t += 4) {
+        const int which = t / (nt * 4), tt = t - which * nt * 4;
+        const int ti = tt >> 2, tj = tt & 3;
+        const bf16_t* X = which == 0 ? dS : which == 1 ? dST : PT;
+        const bf16_t* Y = which == 0 ? KT : which == 1 ? QT : dOT;
+        const f32x4 r = mfma_tile(X, AB_KP, Y, AB_KP, ti, tj, nkk, lane);
+        const int col = which * D + h * 64 + tj * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = ti * 16 + 4 * (lane >> 4) + q;
+            if (i < L) dqkv[(size_t)(b * L + i) * ld + col] = f2bf(r[q]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Token-embedding gradient, deterministic: (id, row) pairs sorted by id (stable radix sort), one
+// workgroup per run of equal ids sums its rows in row order.  Positional gradient: sum over batch.
+__global__ __launch_bounds__(256) void iota_ids_k(int* __restrict__ keys, int* __restrict__ vals,
+                                                  const int64_t* __restrict__ ids, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        keys[i] = (int)ids[i];
+        vals[i] = i;
+    }
+}
+template <int NC>
+__global__ __launch_bounds__(256) void embed_runs_k(float* __restrict__ dtok, const int* __restrict__ keys,
+                                                    const int* __restrict__ rows, const float* __restrict__ dx, int n) {
+    const int i = blockIdx.x;
+    if (i >= n || (i > 0 && keys[i] == keys[i - 1])) return;
+    const int id = keys[i];
+    constexpr int D = NC * 256;
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+    for (int k = i; k < n && keys[k] == id; ++k) {
+        const float* src = dx + (size_t)rows[k] * D;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += src[c * 256 + threadIdx.x];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dtok[(size_t)id * D + c * 256 + threadIdx.x] = acc[c];
+}
+// dpos[t][e] = sum_b dx[b*ctx + t][e]
+__global__ __launch_bounds__(256) void pos_grad_k(float* __restrict__ dpos, const float* __restrict__ dx, int B,
+                                                  int ctx, int D) {
+    const int t = blockIdx.x;
+    for (int e = threadIdx.x; e < D; e += 256) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += dx[((size_t)b * ctx + t) * D + e];
+        dpos[(size_t)t * D + e] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// F.normalize backward: f = u / max(|u|, 1e-12):  du = (df - f (f . df)) / |u|   (|u| > 1e-12)
+__global__ __launch_bounds__(256) void l2norm_bwd_k(float* __restrict__ du, const float* __restrict__ u,
+                                                    const float* __restrict__ df, int rows, int D) {
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const float* ur = u + (size_t)r * D;
+    const float* gr = df + (size_t)r * D;
+    float nn = 0.f;
+    for (int e = lane; e < D; e += 64) nn += ur[e] * ur[e];
+    const float nrm = sqrtf(wave_sum(nn));
+    const float inv = 1.0f / fmaxf(nrm, 1e-12f);
+    float fd = 0.f;
+    for (int e = lane; e < D; e += 64) fd += ur[e] * inv * gr[e];
+    fd = wave_sum(fd);
+    for (int e = lane; e < D; e += 64) {
+        const float f = ur[e] * inv;
+        du[(size_t)r * D + e] = nrm > 1e-12f ? (gr[e] - f * fd) * inv : gr[e] * inv;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross entropy with gradient, one wave per row of logits z [R][C] (z already scaled):
+//   valid row (label >= 0): g = wgt * inv_count * (softmax(z) - onehot(label)),
+//   loss_row = wgt * inv_count * (logsumexp(z) - z[label]),  gz_row = sum_j g_j z_j
+//   ignored row (label -100): g = 0, loss_row = gz_row = 0.
+// g may alias z (in place).  Row partials go to rowstat[2][R] and are summed by ce_finish_k.
+__global__ __launch_bounds__(256) void ce_grad_k(float* __restrict__ g, const float* __restrict__ z, int R, int C,
+                                                 const int64_t* __restrict__ labels, float wgt_inv_count,
+                                                 float* __restrict__ rowstat) {
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const float* zr = z + (size_t)r * C;
+    float* gr = g + (size_t)r * C;
+    const long lab = labels[r];
+    if (lab < 0) {
+        for (int j = lane; j < C; j += 64) gr[j] = 0.f;
+        if (lane == 0) { rowstat[r] = 0.f; rowstat[R + r] = 0.f; }
+        return;
+    }
+    float m = -INFINITY;
+    for (int j = lane; j < C; j += 64) m = fmaxf(m, zr[j]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int j = lane; j < C; j += 64) s += __expf(zr[j] - m);
+    s = wave_sum(s);
+    const float lse = m + __logf(s), is = 1.0f / s;
+    const float zl = zr[lab];
+    float gz = 0.f;
+    for (int j = lane; j < C; j += 64) {
+        const float zj = zr[j];
+        const float gj = wgt_inv_count * (__expf(zj - m) * is - (j == lab ? 1.0f : 0.0f));
+        gz += gj * zj;
+        gr[j] = gj;
+    }
+    gz = wave_sum(gz);
+    if (lane == 0) {
+        rowstat[r] = wgt_inv_count * (lse - zl);
+        rowstat[R + r] = gz;
+    }
+}
+// out[0] += sum_r rowstat[r] (loss), out[1] += sum_r rowstat[R + r] (d loss / d logit_scale)
+__global__ __launch_bounds__(256) void ce_finish_k(float* __restrict__ out, const float* __restrict__ rowstat, int R) {
+    __shared__ float red[2][4];
+    float a = 0.f, c = 0.f;
+    for (int r = threadIdx.x; r < R; r += 256) {
+        a += rowstat[r];
+        c += rowstat[R + r];
+    }
+    a = wave_sum(a);
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        out[1] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// AdamW (torch.optim.AdamW, maximize=False, amsgrad=False), f32 master weights:
+//   p *= 1 - lr*wd;  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;
+//   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+__global__ __launch_bounds__(256) void adamw_k(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ m, float* __restrict__ v, long n, float lr,
+                                               float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i];
+    float pi = p[i] * (1.0f - lr * wd);
+    const float mi = b1 * m[i] + (1.0f - b1) * gi;
+    const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+}
+
+// Engine weight copy from an f32 master: rows < scale_rows are multiplied by `scale` (the q
+// rows of in_proj carry the attention scale, capi.hip ce_load_weights), output f32 or bf16.
+template <bool BF16>
+__global__ __launch_bounds__(256) void weight_from_master_k(void* __restrict__ out, const float* __restrict__ src,
+                                                            long n, long row_len, long scale_rows, float scale) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float x = src[i];
+    if (i / row_len < scale_rows) x *= scale;
+    if constexpr (BF16) static_cast<bf16_t*>(out)[i] = f2bf(x);
+    else static_cast<float*>(out)[i] = x;
+}
+
+__global__ __launch_bounds__(256) void scale_k(float* __restrict__ x, long n, float s) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] *= s;
+}
+
+__global__ __launch_bounds__(256) void axpy_k(float* __restrict__ y, const float* __restrict__ x, long n, float a) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[i] += a * x[i];
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in, long n) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = f2bf(in[i]);
+}
+
+unsigned blocks(long n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+// ============================================================================================
+hipError_t launch_transpose_bf16(bf16_t* out, long ldo, const void* in, bool in_f32, long ldi, int R, int C, int Rpad,
+                                 hipStream_t s) {
+    if (R <= 0 || C <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((std::max(R, Rpad) + 63) / 64), (unsigned)((C + 63) / 64));
+    if (in_f32) hipLaunchKernelGGL((transpose_k<float, bf16_t>), grid, dim3(256), 0, s, out, ldo, (const float*)in, ldi, R, C, Rpad);
+    else hipLaunchKernelGGL((transpose_k<bf16_t, bf16_t>), grid, dim3(256), 0, s, out, ldo, (const bf16_t*)in, ldi, R, C, Rpad);
+    return hipGetLastError();
+}
+hipError_t launch_transpose_f32(float* out, long ldo, const float* in, long ldi, int R, int C, hipStream_t s) {
+    if (R <= 0 || C <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((R + 63) / 64), (unsigned)((C + 63) / 64));
+    hipLaunchKernelGGL((transpose_k<float, float>), grid, dim3(256), 0, s, out, ldo, in, ldi, R, C, R);
+    return hipGetLastError();
+}
+
+long colsum_scratch_floats(int M, int N) { return (long)((M + CS - 1) / CS) * N; }
+hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M, int N, float scale, bool accumulate,
+                         float* scratch, hipStream_t s) {
+    if (N <= 0) return hipSuccess;
+    const int nb = std::max(1, (M + CS - 1) / CS);
+    if (M > 0) {
+        const dim3 grid(blocks(N), (unsigned)nb);
+        if (in_f32) hipLaunchKernelGGL(colsum_part_k<float>, grid, dim3(256), 0, s, scratch, (const float*)in, ld, M, N);
+        else hipLaunchKernelGGL(colsum_part_k<bf16_t>, grid, dim3(256), 0, s, scratch, (const bf16_t*)in, ld, M, N);
+    } else {
+        (void)hipMemsetAsync(scratch, 0, sizeof(float) * N, s);
+    }
+    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(N)), dim3(256), 0, s, out, scratch, nb, N, scale, accumulate ? 1 : 0);
+    return hipGetLastError();
+}
+
+long ln_bwd_scratch_floats(int n, int D) { return 2L * ((n + LNB_ROWS - 1) / LNB_ROWS) * D; }
+hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
+                         int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
+                         hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int nb = (n + LNB_ROWS - 1) / LNB_ROWS;
+    float* pw = scratch;
+    float* pb = scratch + (size_t)nb * D;
+    const int acc = accumulate_dx ? 1 : 0;
+    if (D == 768) hipLaunchKernelGGL(ln_bwd_k<3>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
+    else if (D == 1024) hipLaunchKernelGGL(ln_bwd_k<4>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
+    else if (D == 512) hipLaunchKernelGGL(ln_bwd_k<2>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
+    else return hipErrorInvalidValue;
+    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(D)), dim3(256), 0, s, dw, pw, nb, D, 1.0f, accumulate_dwb ? 1 : 0);
+    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(D)), dim3(256), 0, s, db, pb, nb, D, 1.0f, accumulate_dwb ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s) {
+    if (n % 8) return hipErrorInvalidValue;
+    const long n8 = n / 8;
+    const dim3 grid(blocks(n8));
+#define CE_ACT(A_) \
+    if (act == A_) { \
+        if (dh) hipLaunchKernelGGL((act_k<A_, true>), grid, dim3(256), 0, s, out, pre, dh, n8); \
+        else hipLaunchKernelGGL((act_k<A_, false>), grid, dim3(256), 0, s, out, pre, dh, n8); \
+        return hipGetLastError(); }
+    CE_ACT(ACT_GELU) CE_ACT(ACT_QGELU)
+#undef CE_ACT
+    return hipErrorInvalidValue;
+}
+
+constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * 64 + 3 * 64 * AB_KP + 3 * AB_L * AB_KP) * 2 +
+                               (size_t)(AB_L * AB_L + AB_L) * 4;
+hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, int B, int L, int H,
+                                bool causal, hipStream_t s) {
+    if (L <= 0 || L > AB_L || B <= 0) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, L, H,
+                       causal ? 1 : 0);
+    return hipGetLastError();
+}
+
+size_t embed_bwd_scratch_bytes(int n) {
+    size_t tmp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const int*)nullptr, (int*)nullptr, (const int*)nullptr,
+                                             (int*)nullptr, n);
+    return 4 * sizeof(int) * (size_t)n + tmp + 256;
+}
+hipError_t launch_embed_bwd(float* dtok, float* dpos, const float* dx, const int64_t* ids, int B, int ctx, int D,
+                            int vocab, void* scratch, size_t scratch_bytes, hipStream_t s) {
+    const int n = B * ctx;
+    if (n <= 0) return hipSuccess;
+    int* k0 = static_cast<int*>(scratch);
+    int* v0 = k0 + n;
+    int* k1 = v0 + n;
+    int* v1 = k1 + n;
+    void* tmp = v1 + n;
+    size_t tmp_bytes = scratch_bytes - 4 * sizeof(int) * (size_t)n;
+    hipLaunchKernelGGL(iota_ids_k, dim3(blocks(n)), dim3(256), 0, s, k0, v0, ids, n);
+    int bits = 1;
+    while ((1 << bits) < vocab) ++bits;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, v0, v1, n, 0, bits, s);
+    if (e != hipSuccess) return e;
+    (void)hipMemsetAsync(dtok, 0, sizeof(float) * (size_t)vocab * D, s);
+    if (D == 768) hipLaunchKernelGGL(embed_runs_k<3>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
+    else if (D == 512) hipLaunchKernelGGL(embed_runs_k<2>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
+    else if (D == 1024) hipLaunchKernelGGL(embed_runs_k<4>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
+    else return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pos_grad_k, dim3((unsigned)ctx), dim3(256), 0, s, dpos, dx, B, ctx, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_l2norm_bwd(float* du, const float* u, const float* df, int rows, int D, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(l2norm_bwd_k, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, du, u, df, rows, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_ce_grad(float* g, const float* z, int R, int C, const int64_t* labels, float wgt_inv_count,
+                          float* rowstat, float* out2, hipStream_t s) {
+    if (R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ce_grad_k, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, g, z, R, C, labels, wgt_inv_count,
+                       rowstat);
+    hipLaunchKernelGGL(ce_finish_k, dim3(1), dim3(256), 0, s, out2, rowstat, R);
+    return hipGetLastError();
+}
+
+hipError_t launch_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps,
+                        float wd, int step, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const float bc1 = 1.0f - powf(b1, (float)step);
+    const float bc2s = sqrtf(1.0f - powf(b2, (float)step));
+    hipLaunchKernelGGL(adamw_k, dim3(blocks(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2s);
+    return hipGetLastError();
+}
+
+hipError_t launch_weight_from_master(void* out, bool bf16, const float* src, long n, long row_len, long scale_rows,
+                                     float scale, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (bf16) hipLaunchKernelGGL(weight_from_master_k<true>, dim3(blocks(n)), dim3(256), 0, s, out, src, n, row_len, scale_rows, scale);
+    else hipLaunchKernelGGL(weight_from_master_k<false>, dim3(blocks(n)), dim3(256), 0, s, out, src, n, row_len, scale_rows, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale(float* x, long n, float sc, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scale_k, dim3(blocks(n)), dim3(256), 0, s, x, n, sc);
+    return hipGetLastError();
+}
+
+hipError_t launch_axpy(float* y, const float* x, long n, float a, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(axpy_k, dim3(blocks(n)), dim3(256), 0, s, y, x, n, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cast_bf16(bf16_t* out, const float* in, long n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cast_f32_bf16_k, dim3(blocks(n)), dim3(256), 0, s, out, in, n);
+    return hipGetLastError();
+}
+
+}  // namespace ce

@@ -254,6 +254,33 @@ int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, 
 int ce_kernel_layernorm(void* stream, const float* in, void* out, int out_dtype, const float* w,
                         const float* b, int rows, int D);
 
+/* ---- Text-tower training: the open_clip NegCLIP step with a locked image tower
+ * (open_clip_train/train.py:85-189, main.py:271-302; train-clip.sh: --lock-image --local-loss
+ * --gather-with-grad [--usehardtext]).  The caller owns f32 master values and gradient slots
+ * (device buffers, e.g. views of flat torch tensors so RCCL can all-reduce them in one call):
+ *
+ *   ce_train_bind          every text tensor (token_embedding.weight, positional_embedding,
+ *                          transformer.resblocks.*, ln_final.*, text_projection) -> {param, grad}
+ *   ce_train_sync_weights  engine compute copies (bf16 matrices, f32 vectors) <- masters
+ *   ce_text_forward_train  CLIP.encode_text(normalize=True) keeping the activations the
+ *                          backward needs; out_features [B][embed] f32 (nullable)
+ *   ce_text_backward       d loss / d features [B][embed] -> every bound gradient slot
+ *                          (overwritten), through F.normalize, projection, ln_final on the EOT
+ *                          rows, the blocks (attention: causal, context <= 80) and the embeddings
+ *   ce_contrastive_grad    z = scale A B^T; CE over rows (labels -100 ignored, loss.py:127-135);
+ *                          out2[0] += weight * inv_count * sum CE, out2[1] += sum G o z
+ *                          (= d loss / d logit_scale); dA += scale G B, dB += scale G^T A
+ *                          (nullable), G = weight * inv_count * (softmax - onehot)
+ *   ce_adamw               torch.optim.AdamW over one flat f32 group (step counts from 1) */
+int ce_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* grads, int n);
+int ce_train_sync_weights(ce_handle* h, void* stream);
+int ce_text_forward_train(ce_handle* h, void* stream, const int64_t* ids, int B, float* out_features);
+int ce_text_backward(ce_handle* h, void* stream, const float* d_features, int B);
+int ce_contrastive_grad(ce_handle* h, void* stream, const float* A, int Ra, const float* B, int Cb, int E, float scale,
+                        const int64_t* labels, float weight, float inv_count, float* out2, float* dA, float* dB);
+int ce_adamw(void* stream, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+             float beta1, float beta2, float eps, float weight_decay, int step);
+
 /* ---- CLIP BPE tokenizer (host; replaces open_clip SimpleTokenizer, tokenizer.py:133-265) ----
  * `merges` is the DECOMPRESSED text of bpe_simple_vocab_16e6.txt.gz (tokenizer.py:144: header
  * line, then "a b" merge lines); extra specials follow <start_of_text>, <end_of_text>

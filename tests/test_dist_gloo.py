@@ -65,3 +65,61 @@ def test_negclip_exchange_two_ranks(golden):
     for r in range(2):
         for k in ("hard", "plain_local", "plain_global"):
             np.testing.assert_allclose(got[r][k], float(g[f"{k}_r{r}"]), rtol=1e-5, err_msg=f"{k} rank {r}")
+
+
+def _train_worker(rank, world, port, q):
+    """negclip_feature_grad (the trainer's exchange + gradient bookkeeping) with a torch test double
+    for the engine's ce_contrastive_grad, against the reference's autograd through its 2-rank
+    ClipLoss(local_loss, gather_with_grad, usehardtext) (tests/golden/train_dist.npz)."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "clip-embeds_amd"), repo]
+    from clipembed.train import negclip_feature_grad
+
+    g = dict(np.load(os.path.join(repo, "tests", "golden", "train_dist.npz")))
+    acc = torch.zeros(2, dtype=torch.float64)
+
+    def cgrad(a, b, scale, labels, inv_count, da, db, weight):   # f64 restatement of ce_contrastive_grad
+        a64, b64 = a.double(), b.double()
+        z = scale * a64 @ b64.T
+        p = torch.softmax(z, dim=1)
+        valid = labels >= 0
+        onehot = torch.zeros_like(z)
+        onehot[valid, labels[valid]] = 1.0
+        gz = weight * inv_count * (p - onehot) * valid[:, None]
+        lse = torch.logsumexp(z, dim=1)
+        zl = z.gather(1, labels.clamp(min=0)[:, None])[:, 0]
+        acc[0] += (weight * inv_count * (lse - zl) * valid).sum()
+        acc[1] += (gz * z).sum()
+        if da is not None:
+            da += (scale * gz @ b64).to(da.dtype)
+        if db is not None:
+            db += (scale * gz.T @ a64).to(db.dtype)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    img = torch.from_numpy(g[f"img_r{rank}"])
+    txt = torch.from_numpy(g[f"txt_r{rank}"])
+    dtxt = negclip_feature_grad(img, txt, 12.5, rank, world, cgrad)
+    q.put((rank, {"dtxt": dtxt.numpy(), "loss": float(acc[0]), "dlogit_scale": float(acc[1])}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_feature_grad_two_ranks(golden):
+    g = golden("train_dist")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        np.testing.assert_allclose(got[r]["loss"], float(g[f"loss_r{r}"]), rtol=1e-5)
+        # d loss / d logit_scale = scale * d loss / d scale (the reference differentiates w.r.t. scale)
+        np.testing.assert_allclose(got[r]["dlogit_scale"], 12.5 * float(g[f"dscale_r{r}"]), rtol=1e-4)
+        np.testing.assert_allclose(got[r]["dtxt"], g[f"dtxt_r{r}"], rtol=1e-4, atol=1e-7)
