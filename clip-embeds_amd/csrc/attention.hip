@@ -45,7 +45,7 @@ __device__ __forceinline__ void barrier() {
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int L, int H,
-                                                    float qscale) {
+                                                    float qscale, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
@@ -247,6 +247,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
     const float inv = 1.0f / l_tot;
+    // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
+    if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * L + qrow] = m_run + __log2f(l_tot);
     if (qrow < L) {
         bf16_t* op = out + ((size_t)b * L + qrow) * D + h * 64;
 #pragma unroll
@@ -265,14 +267,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 }  // namespace
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s) {
+                            hipStream_t s, float* lse) {
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
     if (causal)
-        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, qscale);
+        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse);
     else
-        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, qscale);
+        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse);
     return hipGetLastError();
 }
 

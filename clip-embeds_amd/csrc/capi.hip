@@ -572,6 +572,7 @@ struct TrainWs {
     int B = 0, M = 0, Mp = 0, D = 0, F = 0, E = 0, nl = 0;
     std::vector<float*> X, XM;
     std::vector<bf16_t*> xn1, qkv, att, xn2, pre, hh;
+    std::vector<float*> lse;     // [B][H][L] attention row log-sum-exp (log2 units) per layer
     int64_t* ids;
     int* rows;
     float *pooled, *u, *f;
@@ -605,6 +606,7 @@ size_t train_layout(const ce_handle* h, int B, TrainWs* w, char* base) {
         t.xn2.push_back((bf16_t*)take(M * D * 2));
         t.pre.push_back((bf16_t*)take(M * F * 2));
         t.hh.push_back((bf16_t*)take(M * F * 2));
+        t.lse.push_back((float*)take(M * c.text.heads * 4));
     }
     t.ids = (int64_t*)take(M * 8);
     t.rows = (int*)take(B * 4);
@@ -625,7 +627,7 @@ size_t train_layout(const ce_handle* h, int B, TrainWs* w, char* base) {
     t.TB = (bf16_t*)take(NX * Mp * 2);
     t.WT = (bf16_t*)take(NX * D * 2);
     t.part = (float*)take(ce::kGemmPartElems * 4);
-    t.emb_bytes = ce::embed_bwd_scratch_bytes((int)M);
+    t.emb_bytes = ce::embed_bwd_scratch_bytes(B, L, D);
     t.emb = take(t.emb_bytes);
     if (w) *w = t;
     return off;
@@ -676,32 +678,32 @@ int run_text_train(ce_handle* h, hipStream_t s, TrainWs& w, const int64_t* ids) 
     const ce_config& c = h->cfg;
     const int D = w.D, F = w.F, L = c.context_length, H = c.text.heads, M = w.M, B = w.B;
     HIP_TRY(hipMemcpyAsync(w.ids, ids, (size_t)M * 8, hipMemcpyDeviceToDevice, s));
-    CE_TRY(check_launch(ce::launch_text_embed(w.X[0], w.ids, W(h, "token_embedding.weight"), W(h, "positional_embedding"),
-                                              B, L, D, c.vocab_size, s), "token_embedding"));
+    CE_TRY(timed(h, s, "t_token_embedding", 0.0, 0.0, [&] { return ce::launch_text_embed(w.X[0], w.ids, W(h, "token_embedding.weight"), W(h, "positional_embedding"),
+                                              B, L, D, c.vocab_size, s); }));
     for (int l = 0; l < w.nl; ++l) {
         const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(l) + ".");
         CE_TRY(layernorm(h, s, "ln_t", w.X[l], w.xn1[l], true, k.ln1w, k.ln1b, M, D));
         CE_TRY(tgemm(h, s, "train_qkv", w.xn1[l], D, k.wqkv, D, M, 3 * D, D, k.bqkv, ce::ACT_NONE_, nullptr, w.qkv[l],
                      true, w.part));
         CE_TRY(timed(h, s, "train_attn", 4.0 * B * H * (double)L * L * 64, 0.0,
-                     [&] { return ce::launch_attention(w.qkv[l], w.att[l], B, L, H, true, true, s); }));
+                     [&] { return ce::launch_attention(w.qkv[l], w.att[l], B, L, H, true, true, s, w.lse[l]); }));
         CE_TRY(tgemm(h, s, "train_out", w.att[l], D, k.wout, D, M, D, D, k.bout, ce::ACT_NONE_, w.X[l], w.XM[l], false,
                      w.part));
         CE_TRY(layernorm(h, s, "ln_t", w.XM[l], w.xn2[l], true, k.ln2w, k.ln2b, M, D));
         CE_TRY(tgemm(h, s, "train_fc", w.xn2[l], D, k.wfc, D, M, F, D, k.bfc, ce::ACT_NONE_, nullptr, w.pre[l], true,
                      w.part));
-        CE_TRY(check_launch(ce::launch_act(w.hh[l], w.pre[l], nullptr, (long)M * F, act_code(h), s), "act"));
+        CE_TRY(timed(h, s, "t_act", 0.0, 0.0, [&] { return ce::launch_act(w.hh[l], w.pre[l], nullptr, (long)M * F, act_code(h), s); }));
         CE_TRY(tgemm(h, s, "train_proj", w.hh[l], F, k.wproj, F, M, D, F, k.bproj, ce::ACT_NONE_, w.XM[l], w.X[l + 1],
                      false, w.part));
     }
-    CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, w.ids, B, L, s), "argmax"));
-    CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.X[w.nl], w.rows, D, B, D, W(h, "ln_final.weight"),
-                                             W(h, "ln_final.bias"), s), "ln_final(pool)"));
+    CE_TRY(timed(h, s, "t_argmax", 0.0, 0.0, [&] { return ce::launch_argmax_rows(w.rows, w.ids, B, L, s); }));
+    CE_TRY(timed(h, s, "t_ln_final_pool", 0.0, 0.0, [&] { return ce::launch_ln_gather(w.pooled, w.X[w.nl], w.rows, D, B, D, W(h, "ln_final.weight"),
+                                             W(h, "ln_final.bias"), s); }));
     ce::FGemmParams fp{};
     fp.A = w.pooled; fp.lda = D; fp.B = W(h, "text_projection"); fp.ldb = w.E;
     fp.C = w.u; fp.ldc = w.E; fp.M = B; fp.N = w.E; fp.K = D; fp.batch = 1; fp.alpha = 1.f;
-    CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "text_projection"));
-    CE_TRY(check_launch(ce::launch_l2norm(w.f, w.u, B, w.E, s), "normalize"));
+    CE_TRY(timed(h, s, "t_text_projection", 0.0, 0.0, [&] { return ce::launch_fgemm(fp, false, s); }));
+    CE_TRY(timed(h, s, "t_normalize", 0.0, 0.0, [&] { return ce::launch_l2norm(w.f, w.u, B, w.E, s); }));
     return CE_OK;
 }
 
@@ -711,79 +713,75 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
     const int D = w.D, F = w.F, E = w.E, L = c.context_length, H = c.text.heads, M = w.M, Mp = w.Mp, B = w.B;
     const int act = act_code(h);
     // F.normalize, projection, ln_final on the EOT rows (transformer.py:839-855, model.py:300)
-    CE_TRY(check_launch(ce::launch_l2norm_bwd(w.du, w.u, dfeat, B, E, s), "l2norm_bwd"));
-    CE_TRY(check_launch(ce::launch_transpose_f32(w.pooledT, B, w.pooled, D, B, D, s), "transpose"));
+    CE_TRY(timed(h, s, "t_l2norm_bwd", 0.0, 0.0, [&] { return ce::launch_l2norm_bwd(w.du, w.u, dfeat, B, E, s); }));
+    CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_f32(w.pooledT, B, w.pooled, D, B, D, s); }));
     {
         ce::FGemmParams fp{};      // d text_projection [D][E] = pooled^T du
         fp.A = w.pooledT; fp.lda = B; fp.B = w.du; fp.ldb = E; fp.C = grad_of(h, "text_projection"); fp.ldc = E;
         fp.M = D; fp.N = E; fp.K = B; fp.batch = 1; fp.alpha = 1.f;
-        CE_TRY(check_launch(ce::launch_fgemm(fp, false, s), "d_text_projection"));
+        CE_TRY(timed(h, s, "t_d_text_projection", 0.0, 0.0, [&] { return ce::launch_fgemm(fp, false, s); }));
         ce::FGemmParams fq{};      // d pooled [B][D] = du proj^T
         fq.A = w.du; fq.lda = E; fq.B = W(h, "text_projection"); fq.ldb = E; fq.C = w.dpool; fq.ldc = D;
         fq.M = B; fq.N = D; fq.K = E; fq.batch = 1; fq.alpha = 1.f;
-        CE_TRY(check_launch(ce::launch_fgemm(fq, true, s), "d_pooled"));
+        CE_TRY(timed(h, s, "t_d_pooled", 0.0, 0.0, [&] { return ce::launch_fgemm(fq, true, s); }));
     }
     HIP_TRY(hipMemsetAsync(w.dres, 0, (size_t)M * D * 4, s));
-    CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.X[w.nl], w.dpool, D, W(h, "ln_final.weight"), w.rows, B, D,
+    CE_TRY(timed(h, s, "t_ln_final_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[w.nl], w.dpool, D, W(h, "ln_final.weight"), w.rows, B, D,
                                           grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
-                                          w.lnscr, s), "ln_final_bwd"));
+                                          w.lnscr, s); }));
     const float qs = ce::kAttnQScale;
     for (int l = w.nl - 1; l >= 0; --l) {
         const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
         const Blk k = block_ptrs(h, pfx);
         auto G = [&](const char* n) { return grad_of(h, pfx + n); };
         // ---- MLP: X[l+1] = XM + c_proj(act(c_fc(ln_2 XM)))  (transformer.py:235-239, 267) ----
-        CE_TRY(check_launch(ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s), "cast"));
-        CE_TRY(check_launch(ce::launch_colsum(G("mlp.c_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s),
-                            "colsum"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s), "transpose"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s), "transpose"));
+        CE_TRY(timed(h, s, "t_cast", 0.0, 0.0, [&] { return ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s); }));
+        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("mlp.c_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_proj", w.TA, Mp, w.TB, Mp, D, F, Mp, nullptr, 0, nullptr, G("mlp.c_proj.weight"), false,
                      w.part));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s), "transpose"));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s); }));
         CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
-        CE_TRY(check_launch(ce::launch_act(w.dA, w.pre[l], w.dA, (long)M * F, act, s), "act_bwd"));
-        CE_TRY(check_launch(ce::launch_colsum(G("mlp.c_fc.bias"), w.dA, false, F, M, F, 1.f, false, w.colsum, s),
-                            "colsum"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s), "transpose"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] { return ce::launch_act(w.dA, w.pre[l], w.dA, (long)M * F, act, s); }));
+        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("mlp.c_fc.bias"), w.dA, false, F, M, F, 1.f, false, w.colsum, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_fc", w.TA, Mp, w.TB, Mp, F, D, Mp, nullptr, 0, nullptr, G("mlp.c_fc.weight"), false,
                      w.part));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s), "transpose"));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s); }));
         CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, w.dxn, false, w.part));
-        CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
-                                              G("ln_2.bias"), true, false, w.lnscr, s), "ln_2_bwd"));
+        CE_TRY(timed(h, s, "t_ln_2_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
+                                              G("ln_2.bias"), true, false, w.lnscr, s); }));
         // ---- attention: XM = X + out_proj(MHA(ln_1 X))  (transformer.py:242-255, 266) ----
-        CE_TRY(check_launch(ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s), "cast"));
-        CE_TRY(check_launch(ce::launch_colsum(G("attn.out_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s),
-                            "colsum"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s), "transpose"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(timed(h, s, "t_cast", 0.0, 0.0, [&] { return ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s); }));
+        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("attn.out_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_out", w.TA, Mp, w.TB, Mp, D, D, Mp, nullptr, 0, nullptr, G("attn.out_proj.weight"),
                      false, w.part));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, D, k.wout, false, D, D, D, D, s), "transpose"));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wout, false, D, D, D, D, s); }));
         CE_TRY(tgemm(h, s, "dX_out", w.dres_b, D, w.WT, D, M, D, D, nullptr, 0, nullptr, w.dB, true, w.part));
         CE_TRY(timed(h, s, "attn_bwd", 10.0 * B * H * (double)L * L * 64, 0.0, [&] {
-            return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, B, L, H, true, s);
+            return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, w.lse[l], B, L, H, true, s);
         }));
         // in_proj: the engine's q rows carry kAttnQScale, so d(master q rows) = qs * d(engine q rows)
-        CE_TRY(check_launch(ce::launch_colsum(G("attn.in_proj_bias"), w.dA, false, 3 * D, M, 3 * D, 1.f, false,
-                                              w.colsum, s), "colsum"));
-        CE_TRY(check_launch(ce::launch_scale(G("attn.in_proj_bias"), D, qs, s), "scale"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s), "transpose"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s), "transpose"));
+        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("attn.in_proj_bias"), w.dA, false, 3 * D, M, 3 * D, 1.f, false,
+                                              w.colsum, s); }));
+        CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_bias"), D, qs, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_qkv", w.TA, Mp, w.TB, Mp, 3 * D, D, Mp, nullptr, 0, nullptr, G("attn.in_proj_weight"),
                      false, w.part));
-        CE_TRY(check_launch(ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s), "scale"));
-        CE_TRY(check_launch(ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s),
-                            "transpose"));
+        CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s); }));
+        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s); }));
         CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, w.dxn, false, w.part));
-        CE_TRY(check_launch(ce::launch_ln_bwd(w.dres, w.X[l], w.dxn, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
-                                              G("ln_1.bias"), true, false, w.lnscr, s), "ln_1_bwd"));
+        CE_TRY(timed(h, s, "t_ln_1_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[l], w.dxn, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
+                                              G("ln_1.bias"), true, false, w.lnscr, s); }));
     }
     // token / positional embeddings (model.py:286-288)
-    CE_TRY(check_launch(ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),
-                                             w.dres, w.ids, B, L, D, c.vocab_size, w.emb, w.emb_bytes, s), "embed_bwd"));
+    CE_TRY(timed(h, s, "t_embed_bwd", 0.0, 0.0, [&] { return ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),
+                                             w.dres, w.ids, B, L, D, c.vocab_size, w.emb, w.emb_bytes, s); }));
     return CE_OK;
 }
 

@@ -40,7 +40,7 @@ constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a 
 // kernel scales its Q fragments.
 constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(64)
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s);
+                            hipStream_t s, float* lse = nullptr);   // lse: [B][H][L] log2 log-sum-exp (training)
 
 // LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.
 //   in row  = (r / grp) * i_gs + i_go + r % grp   (grp == 0: identity)
@@ -142,10 +142,10 @@ hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy,
 // dh == nullptr: out = act(pre); else out = dh * act'(pre).  bf16, n % 8 == 0.
 hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s);
 // attention backward (L <= 80): dqkv [B*L][3*H*64] from qkv (q pre-scaled), O, dO [B*L][H*64]
-hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, int B, int L, int H,
-                                bool causal, hipStream_t s);
+hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
+                                int B, int L, int H, bool causal, hipStream_t s);
 // token / positional embedding gradients from dx [B*ctx][D] (dtok fully overwritten)
-size_t embed_bwd_scratch_bytes(int n);
+size_t embed_bwd_scratch_bytes(int B, int ctx, int D);
 hipError_t launch_embed_bwd(float* dtok, float* dpos, const float* dx, const int64_t* ids, int B, int ctx, int D,
                             int vocab, void* scratch, size_t scratch_bytes, hipStream_t s);
 hipError_t launch_l2norm_bwd(float* du, const float* u, const float* df, int rows, int D, hipStream_t s);

@@ -51,26 +51,43 @@ __global__ __launch_bounds__(256) void transpose_k(TO* __restrict__ out, long ld
 }
 
 // ---------------------------------------------------------------------------------------------
-// Column sums, deterministic two-stage: part[blk][n] = sum of rows blk*CS .. +CS-1, then
-// out[n] = scale * sum_blk part[blk][n] (+ out[n] when accumulate).
-constexpr int CS = 256;
+// Column sums, deterministic two-stage: part[blk][n] = sum of rows [blk*cs, (blk+1)*cs), then
+// out[n] = scale * sum_blk part[blk][n] (+ out[n] when accumulate).  Blocks of 64 columns x 4 row
+// lanes (a wave reads 64 consecutive columns of one row), fixed summation order.
 template <typename TI>
 __global__ __launch_bounds__(256) void colsum_part_k(float* __restrict__ part, const TI* __restrict__ in, long ld,
-                                                     int M, int N) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n >= N) return;
-    const int m0 = blockIdx.y * CS, m1 = min(M, m0 + CS);
-    float s = 0.f;
-    for (int m = m0; m < m1; ++m) s += ld_f(in + (size_t)m * ld + n);
-    part[(size_t)blockIdx.y * N + n] = s;
+                                                     int M, int N, int cs) {
+    __shared__ float red[4][64];
+    const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    const int n = blockIdx.x * 64 + c;
+    const int m0 = blockIdx.y * cs, m1 = min(M, m0 + cs);
+    float a0 = 0.f, a1 = 0.f;
+    if (n < N) {
+        int m = m0 + r4;
+        for (; m + 4 < m1; m += 8) {
+            a0 += ld_f(in + (size_t)m * ld + n);
+            a1 += ld_f(in + (size_t)(m + 4) * ld + n);
+        }
+        if (m < m1) a0 += ld_f(in + (size_t)m * ld + n);
+    }
+    red[r4][c] = a0 + a1;
+    __syncthreads();
+    if (r4 == 0 && n < N) part[(size_t)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, const float* __restrict__ part,
                                                        int nb, int N, float scale, int accumulate) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n >= N) return;
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += part[(size_t)b * N + n];
-    out[n] = (accumulate ? out[n] : 0.f) + scale * s;
+    __shared__ float red[4][64];
+    const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    const int n = blockIdx.x * 64 + c;
+    float a = 0.f;
+    if (n < N)
+        for (int b = r4; b < nb; b += 4) a += part[(size_t)b * N + n];
+    red[r4][c] = a;
+    __syncthreads();
+    if (r4 == 0 && n < N) {
+        const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+        out[n] = (accumulate ? out[n] : 0.f) + scale * s;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -78,7 +95,7 @@ __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, 
 //   xh = (x - mu) * rstd;  g = dy * w;  dx = rstd * (g - mean(g) - xh * mean(g * xh))
 //   dres[row] (+)= dx;  part_w[blk] += dy * xh;  part_b[blk] += dy
 // rows != null: x and dres rows are rows[i] (EOT pooling), dy row is i.
-constexpr int LNB_ROWS = 64;   // rows per block (partial dw/db per block)
+constexpr int LNB_ROWS = 16;   // rows per block (partial dw/db per block)
 template <int NC>
 __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const float* __restrict__ x,
                                                 const float* __restrict__ dy, long ldy, const float* __restrict__ w,
@@ -185,13 +202,14 @@ __global__ __launch_bounds__(256) void act_k(bf16_t* __restrict__ out, const bf1
 // ---------------------------------------------------------------------------------------------
 // Attention backward for one (batch, head) per workgroup, L <= 80 (the text context, 77), d = 64,
 // on MFMA (v_mfma_f32_16x16x32_bf16).  q arrives pre-scaled (q' = q * log2(e)/8: the forward's
-// convention, attention.hip), so S = q' k^T is in log2 units and P = exp2(S - m) / Z.  With
-// delta_i = dO_i . O_i (O = the forward output):
+// convention, attention.hip), so S = q' k^T is in log2 units and, with the forward's row
+// log-sum-exp lse (log2 units), P = exp2(S - lse) tile by tile -- no row pass.  delta_i = dO_i . O_i:
 //   dP = dO V^T;  dS = ln2 * P o (dP - delta);  dq' = dS K;  dk = dS^T q';  dv = P^T dO
 // dq' is the gradient w.r.t. the stored (pre-scaled) q; the in_proj chain rule is applied by the
-// caller.  LDS: row-major q', k, v, dO [80][64]; transposed q'^T, k^T, dO^T [64][96]; P^T, dS, dS^T
-// [80][96] bf16 (contraction dims zero-padded to 96 = 3 x 32); S/P f32 [80][80].
-constexpr int AB_L = 80, AB_KP = 96;
+// caller.  LDS (bf16): row-major q', k, v, dO [80][AB_LD]; transposed q'^T, k^T, dO^T [64][AB_LT];
+// P^T, dS, dS^T [80][AB_LT] (contraction dims zero-padded to 96 = 3 x 32).  Row strides are padded
+// (72 / 104 elements) so the 16 rows a ds_read_b128 lane group touches fall in distinct banks.
+constexpr int AB_L = 80, AB_KP = 96, AB_LD = 72, AB_LT = 104;
 __device__ __forceinline__ bf16x8 lds_frag(const bf16_t* base, int ld, int row, int k0) {
     return *reinterpret_cast<const bf16x8*>(base + row * ld + k0);
 }
@@ -211,26 +229,28 @@ __device__ __forceinline__ f32x4 mfma_tile(const bf16_t* X, int ldx, const bf16_
 
 __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ qkv,
                                                   const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                  int L, int H, int causal) {
+                                                  const float* __restrict__ lse, int L, int H, int causal) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][64]
-    bf16_t* Ks = Qs + AB_L * 64;
-    bf16_t* Vs = Ks + AB_L * 64;
-    bf16_t* dOs = Vs + AB_L * 64;
-    bf16_t* QT = dOs + AB_L * 64;                            // [64][96]
-    bf16_t* KT = QT + 64 * AB_KP;
-    bf16_t* dOT = KT + 64 * AB_KP;
-    bf16_t* PT = dOT + 64 * AB_KP;                           // [80][96]
-    bf16_t* dS = PT + AB_L * AB_KP;
-    bf16_t* dST = dS + AB_L * AB_KP;
-    float* Sf = reinterpret_cast<float*>(dST + AB_L * AB_KP);  // [80][80]
-    float* delta = Sf + AB_L * AB_L;                          // [80]
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][AB_LD]
+    bf16_t* Ks = Qs + AB_L * AB_LD;
+    bf16_t* Vs = Ks + AB_L * AB_LD;
+    bf16_t* dOs = Vs + AB_L * AB_LD;
+    bf16_t* QT = dOs + AB_L * AB_LD;                         // [64][AB_LT]
+    bf16_t* KT = QT + 64 * AB_LT;
+    bf16_t* dOT = KT + 64 * AB_LT;
+    bf16_t* PT = dOT + 64 * AB_LT;                           // [80][AB_LT]
+    bf16_t* dS = PT + AB_L * AB_LT;
+    bf16_t* dST = dS + AB_L * AB_LT;
+    float* delta = reinterpret_cast<float*>(dST + AB_L * AB_LT);   // [80]
+    float* lrow = delta + AB_L;                                     // [80]
 
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int D = H * 64, ld = 3 * D;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // zero the padded operands (rows >= L of the row-major images, columns >= L of the others)
-    for (int e = tid; e < 3 * 64 * AB_KP + 3 * AB_L * AB_KP; e += 256) QT[e] = 0;
+    // zero the transposed / P / dS images (their contraction padding must read as 0)
+    for (int e = tid; e < (3 * 64 * AB_LT + 3 * AB_L * AB_LT) / 8; e += 256)
+        reinterpret_cast<uint4*>(QT)[e] = make_uint4(0, 0, 0, 0);
+    if (tid < AB_L) lrow[tid] = tid < L ? lse[(size_t)bh * L + tid] : 0.f;
     __syncthreads();
     // load q', k, v, dO rows (16 B per thread-chunk) + delta_i = dO_i . O_i
     for (int e = tid; e < AB_L * 8; e += 256) {
@@ -244,10 +264,10 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
             g = *reinterpret_cast<const uint4*>(dO + row * D + h * 64 + c);
             o = *reinterpret_cast<const uint4*>(O + row * D + h * 64 + c);
         }
-        *reinterpret_cast<uint4*>(Qs + i * 64 + c) = q;
-        *reinterpret_cast<uint4*>(Ks + i * 64 + c) = k;
-        *reinterpret_cast<uint4*>(Vs + i * 64 + c) = v;
-        *reinterpret_cast<uint4*>(dOs + i * 64 + c) = g;
+        *reinterpret_cast<uint4*>(Qs + i * AB_LD + c) = q;
+        *reinterpret_cast<uint4*>(Ks + i * AB_LD + c) = k;
+        *reinterpret_cast<uint4*>(Vs + i * AB_LD + c) = v;
+        *reinterpret_cast<uint4*>(dOs + i * AB_LD + c) = g;
         const bf16_t* qs = reinterpret_cast<const bf16_t*>(&q);
         const bf16_t* ks = reinterpret_cast<const bf16_t*>(&k);
         const bf16_t* gs = reinterpret_cast<const bf16_t*>(&g);
@@ -255,12 +275,12 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
         float part = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            QT[(c + t) * AB_KP + i] = qs[t];
-            KT[(c + t) * AB_KP + i] = ks[t];
-            dOT[(c + t) * AB_KP + i] = gs[t];
+            QT[(c + t) * AB_LT + i] = qs[t];
+            KT[(c + t) * AB_LT + i] = ks[t];
+            dOT[(c + t) * AB_LT + i] = gs[t];
             part += bf2f(gs[t]) * bf2f(os[t]);
         }
-        // the 8 chunks of row i are 8 consecutive lanes of one wave
+        // the 8 chunks of row i are 8 consecutive lanes of one wave (640 = 2.5 x 256: whole waves)
         part += __shfl_xor(part, 1, 64);
         part += __shfl_xor(part, 2, 64);
         part += __shfl_xor(part, 4, 64);
@@ -268,44 +288,22 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
     }
     __syncthreads();
     const int nt = (L + 15) / 16;
-    // S = q' k^T (f32, log2 units)
+    // per 16 x 16 tile: S = q' k^T -> P = exp2(S - lse) (masked) -> dP = dO V^T -> dS
     for (int t = wave; t < nt * nt; t += 4) {
         const int ti = t / nt, tj = t - ti * nt;
-        const f32x4 s = mfma_tile(Qs, 64, Ks, 64, ti, tj, 2, lane);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Sf[(ti * 16 + 4 * (lane >> 4) + q) * AB_L + tj * 16 + (lane & 15)] = s[q];
-    }
-    __syncthreads();
-    // row softmax (one wave per row; j < L and, causal, j <= i); P kept f32 in Sf, P^T bf16
-    for (int i = wave; i < L; i += 4) {
-        const int jmax = causal ? i + 1 : L;
-        float m = -INFINITY;
-        for (int j = lane; j < jmax; j += 64) m = fmaxf(m, Sf[i * AB_L + j]);
-        m = wave_max(m);
-        float z = 0.f;
-        for (int j = lane; j < jmax; j += 64) z += exp2f(Sf[i * AB_L + j] - m);
-        z = wave_sum(z);
-        const float iz = 1.0f / z;
-        for (int j = lane; j < AB_L; j += 64) {
-            const float p = j < jmax ? exp2f(Sf[i * AB_L + j] - m) * iz : 0.f;
-            Sf[i * AB_L + j] = p;
-            PT[j * AB_KP + i] = f2bf(p);
-        }
-    }
-    __syncthreads();
-    // dP = dO V^T -> dS = ln2 * P (dP - delta), bf16 both orientations
-    for (int t = wave; t < nt * nt; t += 4) {
-        const int ti = t / nt, tj = t - ti * nt;
-        const f32x4 dp = mfma_tile(dOs, 64, Vs, 64, ti, tj, 2, lane);
+        const f32x4 sv = mfma_tile(Qs, AB_LD, Ks, AB_LD, ti, tj, 2, lane);
+        const f32x4 dp = mfma_tile(dOs, AB_LD, Vs, AB_LD, ti, tj, 2, lane);
         const int j = tj * 16 + (lane & 15);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int i = ti * 16 + 4 * (lane >> 4) + q;
-            const float p = (i < L && j < L) ? Sf[i * AB_L + j] : 0.f;
-            const float ds = 0.69314718055994531f * p * (dp[q] - delta[i < L ? i : 0]);
+            const bool ok = i < L && j < L && !(causal && j > i);
+            const float p = ok ? exp2f(sv[q] - lrow[i]) : 0.f;
+            const float ds = ok ? 0.69314718055994531f * p * (dp[q] - delta[i]) : 0.f;
+            PT[j * AB_LT + i] = f2bf(p);
             const bf16_t v = f2bf(ds);
-            dS[i * AB_KP + j] = v;
-            dST[j * AB_KP + i] = v;
+            dS[i * AB_LT + j] = v;
+            dST[j * AB_LT + i] = v;
         }
     }
     __syncthreads();
@@ -317,7 +315,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
         const int ti = tt >> 2, tj = tt & 3;
         const bf16_t* X = which == 0 ? dS : which == 1 ? dST : PT;
         const bf16_t* Y = which == 0 ? KT : which == 1 ? QT : dOT;
-        const f32x4 r = mfma_tile(X, AB_KP, Y, AB_KP, ti, tj, nkk, lane);
+        const f32x4 r = mfma_tile(X, AB_LT, Y, AB_LT, ti, tj, nkk, lane);
         const int col = which * D + h * 64 + tj * 16 + (lane & 15);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -338,33 +336,58 @@ __global__ __launch_bounds__(256) void iota_ids_k(int* __restrict__ keys, int* _
         vals[i] = i;
     }
 }
+// Runs of equal ids are summed chunk by chunk (ECH sorted positions per workgroup): a run that
+// starts and ends inside a chunk is written to dtok directly; the pieces of runs crossing chunk
+// boundaries go to first[c] (a run continued from before chunk c) / last[c] (a run starting in
+// chunk c that continues), and embed_join_k sums each crossing run's pieces in chunk order.
+constexpr int ECH = 64;
 template <int NC>
-__global__ __launch_bounds__(256) void embed_runs_k(float* __restrict__ dtok, const int* __restrict__ keys,
-                                                    const int* __restrict__ rows, const float* __restrict__ dx, int n) {
-    const int i = blockIdx.x;
-    if (i >= n || (i > 0 && keys[i] == keys[i - 1])) return;
-    const int id = keys[i];
+__global__ __launch_bounds__(256) void embed_pieces_k(float* __restrict__ dtok, float* __restrict__ first,
+                                                      float* __restrict__ last, const int* __restrict__ keys,
+                                                      const int* __restrict__ rows, const float* __restrict__ dx,
+                                                      int n) {
     constexpr int D = NC * 256;
+    const int c = blockIdx.x, c0 = c * ECH, c1 = min(n, c0 + ECH);
+    float acc[NC];
+    int a = c0;
+    while (a < c1) {
+        const int id = keys[a];
+        int b = a;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) acc[q] = 0.f;
+        for (; b < c1 && keys[b] == id; ++b) {
+            const float* src = dx + (size_t)rows[b] * D + threadIdx.x;
+#pragma unroll
+            for (int q = 0; q < NC; ++q) acc[q] += src[q * 256];
+        }
+        const bool starts = a == 0 || keys[a - 1] != id;
+        const bool ends = b >= n || keys[b] != id;
+        float* dst = (starts && ends) ? dtok + (size_t)id * D : (!starts ? first : last) + (size_t)c * D;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) dst[q * 256 + threadIdx.x] = acc[q];
+        a = b;
+    }
+}
+template <int NC>
+__global__ __launch_bounds__(256) void embed_join_k(float* __restrict__ dtok, const float* __restrict__ first,
+                                                    const float* __restrict__ last, const int* __restrict__ keys,
+                                                    int n, int nch) {
+    constexpr int D = NC * 256;
+    const int c = blockIdx.x, c1 = min(n, (c + 1) * ECH);
+    const int id = keys[c1 - 1];
+    // owner: the chunk in which the run of its last position starts, when that run continues
+    if (c1 >= n || keys[c1] != id) return;
+    int a = c1 - 1;
+    while (a > c * ECH && keys[a - 1] == id) --a;
+    if (a == c * ECH && c > 0 && keys[a - 1] == id) return;   // run started in an earlier chunk
     float acc[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] = 0.f;
-    for (int k = i; k < n && keys[k] == id; ++k) {
-        const float* src = dx + (size_t)rows[k] * D;
+    for (int q = 0; q < NC; ++q) acc[q] = last[(size_t)c * D + q * 256 + threadIdx.x];
+    for (int cc = c + 1; cc < nch && keys[cc * ECH] == id; ++cc)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) acc[c] += src[c * 256 + threadIdx.x];
-    }
+        for (int q = 0; q < NC; ++q) acc[q] += first[(size_t)cc * D + q * 256 + threadIdx.x];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) dtok[(size_t)id * D + c * 256 + threadIdx.x] = acc[c];
-}
-// dpos[t][e] = sum_b dx[b*ctx + t][e]
-__global__ __launch_bounds__(256) void pos_grad_k(float* __restrict__ dpos, const float* __restrict__ dx, int B,
-                                                  int ctx, int D) {
-    const int t = blockIdx.x;
-    for (int e = threadIdx.x; e < D; e += 256) {
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) s += dx[((size_t)b * ctx + t) * D + e];
-        dpos[(size_t)t * D + e] = s;
-    }
+    for (int q = 0; q < NC; ++q) dtok[(size_t)id * D + q * 256 + threadIdx.x] = acc[q];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -513,23 +536,38 @@ hipError_t launch_transpose_f32(float* out, long ldo, const float* in, long ldi,
     return hipGetLastError();
 }
 
-long colsum_scratch_floats(int M, int N) { return (long)((M + CS - 1) / CS) * N; }
+int colsum_chunk(int M, int N) {
+    const int colblocks = (N + 63) / 64;
+    const int target = std::max(1, 2048 / colblocks);
+    int cs = (M + target - 1) / target;
+    cs = std::max(64, (cs + 7) / 8 * 8);
+    return cs;
+}
+long colsum_scratch_floats(int M, int N) {
+    const int cs = colsum_chunk(M, N);
+    return (long)std::max(1, (M + cs - 1) / cs) * N;
+}
 hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M, int N, float scale, bool accumulate,
                          float* scratch, hipStream_t s) {
     if (N <= 0) return hipSuccess;
-    const int nb = std::max(1, (M + CS - 1) / CS);
+    const int cs = colsum_chunk(M, N);
+    const int nb = std::max(1, (M + cs - 1) / cs);
+    const unsigned cb = (unsigned)((N + 63) / 64);
     if (M > 0) {
-        const dim3 grid(blocks(N), (unsigned)nb);
-        if (in_f32) hipLaunchKernelGGL(colsum_part_k<float>, grid, dim3(256), 0, s, scratch, (const float*)in, ld, M, N);
-        else hipLaunchKernelGGL(colsum_part_k<bf16_t>, grid, dim3(256), 0, s, scratch, (const bf16_t*)in, ld, M, N);
+        const dim3 grid(cb, (unsigned)nb);
+        if (in_f32) hipLaunchKernelGGL(colsum_part_k<float>, grid, dim3(256), 0, s, scratch, (const float*)in, ld, M, N, cs);
+        else hipLaunchKernelGGL(colsum_part_k<bf16_t>, grid, dim3(256), 0, s, scratch, (const bf16_t*)in, ld, M, N, cs);
     } else {
         (void)hipMemsetAsync(scratch, 0, sizeof(float) * N, s);
     }
-    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(N)), dim3(256), 0, s, out, scratch, nb, N, scale, accumulate ? 1 : 0);
+    hipLaunchKernelGGL(colsum_finish_k, dim3(cb), dim3(256), 0, s, out, scratch, nb, N, scale, accumulate ? 1 : 0);
     return hipGetLastError();
 }
 
-long ln_bwd_scratch_floats(int n, int D) { return 2L * ((n + LNB_ROWS - 1) / LNB_ROWS) * D; }
+long ln_bwd_scratch_floats(int n, int D) {
+    const int nb = (n + LNB_ROWS - 1) / LNB_ROWS;
+    return 2L * nb * D + colsum_scratch_floats(nb, D);
+}
 hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
                          int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
                          hipStream_t s) {
@@ -542,9 +580,10 @@ hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy,
     else if (D == 1024) hipLaunchKernelGGL(ln_bwd_k<4>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
     else if (D == 512) hipLaunchKernelGGL(ln_bwd_k<2>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
     else return hipErrorInvalidValue;
-    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(D)), dim3(256), 0, s, dw, pw, nb, D, 1.0f, accumulate_dwb ? 1 : 0);
-    hipLaunchKernelGGL(colsum_finish_k, dim3(blocks(D)), dim3(256), 0, s, db, pb, nb, D, 1.0f, accumulate_dwb ? 1 : 0);
-    return hipGetLastError();
+    float* cscr = pb + (size_t)nb * D;
+    hipError_t e = launch_colsum(dw, pw, true, D, nb, D, 1.0f, accumulate_dwb, cscr, s);
+    if (e == hipSuccess) e = launch_colsum(db, pb, true, D, nb, D, 1.0f, accumulate_dwb, cscr, s);
+    return e;
 }
 
 hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s) {
@@ -561,49 +600,57 @@ hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, 
     return hipErrorInvalidValue;
 }
 
-constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * 64 + 3 * 64 * AB_KP + 3 * AB_L * AB_KP) * 2 +
-                               (size_t)(AB_L * AB_L + AB_L) * 4;
-hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, int B, int L, int H,
-                                bool causal, hipStream_t s) {
-    if (L <= 0 || L > AB_L || B <= 0) return hipErrorInvalidValue;
+constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * AB_LD + 3 * 64 * AB_LT + 3 * AB_L * AB_LT) * 2 + (size_t)(2 * AB_L) * 4;
+hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
+                                int B, int L, int H, bool causal, hipStream_t s) {
+    if (L <= 0 || L > AB_L || B <= 0 || !lse) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
         attr = true;
     }
-    hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, L, H,
+    hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, lse, L, H,
                        causal ? 1 : 0);
     return hipGetLastError();
 }
 
-size_t embed_bwd_scratch_bytes(int n) {
+size_t embed_bwd_scratch_bytes(int B, int ctx, int D) {
+    const int n = B * ctx, nch = (n + ECH - 1) / ECH;
     size_t tmp = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const int*)nullptr, (int*)nullptr, (const int*)nullptr,
                                              (int*)nullptr, n);
-    return 4 * sizeof(int) * (size_t)n + tmp + 256;
+    return 4 * sizeof(int) * (size_t)n + 2 * sizeof(float) * (size_t)nch * D +
+           sizeof(float) * (size_t)colsum_scratch_floats(B, ctx * D) + tmp + 1024;
 }
 hipError_t launch_embed_bwd(float* dtok, float* dpos, const float* dx, const int64_t* ids, int B, int ctx, int D,
                             int vocab, void* scratch, size_t scratch_bytes, hipStream_t s) {
     const int n = B * ctx;
     if (n <= 0) return hipSuccess;
+    if (D != 512 && D != 768 && D != 1024) return hipErrorInvalidValue;
+    const int nch = (n + ECH - 1) / ECH;
     int* k0 = static_cast<int*>(scratch);
     int* v0 = k0 + n;
     int* k1 = v0 + n;
     int* v1 = k1 + n;
-    void* tmp = v1 + n;
-    size_t tmp_bytes = scratch_bytes - 4 * sizeof(int) * (size_t)n;
+    float* first = reinterpret_cast<float*>(v1 + n);
+    float* last = first + (size_t)nch * D;
+    float* cscr = last + (size_t)nch * D;
+    void* tmp = cscr + colsum_scratch_floats(B, ctx * D);
+    const size_t used = (size_t)((char*)tmp - (char*)scratch);
+    size_t tmp_bytes = scratch_bytes - used;
     hipLaunchKernelGGL(iota_ids_k, dim3(blocks(n)), dim3(256), 0, s, k0, v0, ids, n);
     int bits = 1;
     while ((1 << bits) < vocab) ++bits;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, v0, v1, n, 0, bits, s);
     if (e != hipSuccess) return e;
     (void)hipMemsetAsync(dtok, 0, sizeof(float) * (size_t)vocab * D, s);
-    if (D == 768) hipLaunchKernelGGL(embed_runs_k<3>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
-    else if (D == 512) hipLaunchKernelGGL(embed_runs_k<2>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
-    else if (D == 1024) hipLaunchKernelGGL(embed_runs_k<4>, dim3((unsigned)n), dim3(256), 0, s, dtok, k1, v1, dx, n);
-    else return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pos_grad_k, dim3((unsigned)ctx), dim3(256), 0, s, dpos, dx, B, ctx, D);
-    return hipGetLastError();
+#define CE_EMB(NC_) \
+    hipLaunchKernelGGL(embed_pieces_k<NC_>, dim3((unsigned)nch), dim3(256), 0, s, dtok, first, last, k1, v1, dx, n); \
+    hipLaunchKernelGGL(embed_join_k<NC_>, dim3((unsigned)nch), dim3(256), 0, s, dtok, first, last, k1, n, nch);
+    if (D == 768) { CE_EMB(3) } else if (D == 512) { CE_EMB(2) } else { CE_EMB(4) }
+#undef CE_EMB
+    // positional: column sums of dx viewed as [B][ctx * D]
+    return launch_colsum(dpos, dx, true, (long)ctx * D, B, ctx * D, 1.0f, false, cscr, s);
 }
 
 hipError_t launch_l2norm_bwd(float* du, const float* u, const float* df, int rows, int D, hipStream_t s) {
