@@ -8,7 +8,7 @@ from .config import ModelConfig, get_model_config, list_models
 from .model import CLIP, Engine, create_model, create_model_and_transforms, load_checkpoint_file
 from .train import TextTowerTrainer
 from .tokenizer import SimpleTokenizer, decode, get_tokenizer, tokenize
-from .transforms import image_transform, prepare_data
+from .transforms import image_transform, prepare_data, prepare_data_clip
 from .weights import (synthetic_captions, synthetic_images, synthetic_images_u8, synthetic_pacl_heads,
                       synthetic_state_dict)
 
@@ -17,7 +17,7 @@ __version__ = "0.1.0"
 __all__ = [
     "CLIP", "Engine", "ClipEmbedError", "ModelConfig", "LIB_PATH", "create_model",
     "create_model_and_transforms", "exported_symbols", "get_model_config", "image_transform", "list_models",
-    "load_checkpoint_file", "prepare_data", "synthetic_captions", "synthetic_images", "synthetic_images_u8",
+    "load_checkpoint_file", "prepare_data", "prepare_data_clip", "synthetic_captions", "synthetic_images", "synthetic_images_u8",
     "synthetic_pacl_heads", "synthetic_state_dict", "SimpleTokenizer", "tokenize", "decode", "get_tokenizer",
     "TextTowerTrainer",
 ]

@@ -98,6 +98,13 @@ class Engine:
         _lib.call("ce_missing_weights", self.h, ctypes.byref(n), ctypes.byref(first))
         return n.value, (first.value or b"").decode()
 
+    def set_ln_fold(self, on: bool) -> bool:
+        """Fold the image tower's block LayerNorms into their GEMMs (default on); returns the previous
+        setting.  Takes effect for weights already loaded in whole-block calls (ce_set_ln_fold)."""
+        prev = ctypes.c_int()
+        _lib.call("ce_set_ln_fold", self.h, 1 if on else 0, ctypes.byref(prev))
+        return prev.value == 1
+
     # ---- timing (roofline reporting) ----
     def set_timing(self, on: bool, only: str = ""):
         """Bracket kernel launches with HIP events (all tags, or only the launches tagged `only`)."""

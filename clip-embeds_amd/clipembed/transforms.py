@@ -94,9 +94,27 @@ def image_transform(image_size=336, is_train: bool = False, mean: Optional[Seque
     return DeviceImageProcessor(_lib.CE_PRE_CLIP_BICUBIC, image_size, device, engine=engine)
 
 
-class prepare_data:
-    """PACL prepare_data (data/utils.py:30-52): preprocess_image on the device.  The tokenizer half
-    (open_clip get_tokenizer) stays on the host and is not provided here."""
+class _TextHalf:
+    """preprocess_text of the reference's prepare_data classes (data/utils.py:54-55, 69-70): the
+    ViT-L-14-336 tokenizer, here the C++ CLIP BPE (clipembed.tokenizer).  Created on first use, so
+    the image half works where no BPE vocabulary file is available."""
+
+    _tokenizer = None
+
+    @property
+    def tokenizer(self):
+        if self._tokenizer is None:
+            from .tokenizer import get_tokenizer
+            self._tokenizer = get_tokenizer("ViT-L-14-336")
+        return self._tokenizer
+
+    def preprocess_text(self, caption):
+        return self.tokenizer(caption)
+
+
+class prepare_data(_TextHalf):
+    """PACL prepare_data (data/utils.py:30-55): preprocess_image on the device, preprocess_text
+    through the C++ tokenizer."""
 
     def __init__(self, base_model: str = "ViT-L-14-336", device=None, engine=None):
         if base_model != "ViT-L-14-336":
@@ -105,3 +123,17 @@ class prepare_data:
 
     def preprocess_image(self, image):
         return self.val_transform(image)     # a list -> one batched launch, as torch.stack of the reference
+
+
+class prepare_data_clip(_TextHalf):
+    """prepare_data_clip (data/utils.py:57-70): preprocess_image with the processor returned by
+    create_model_and_transforms (eval_clip.py:21-24).  A DeviceImageProcessor takes a list in one
+    batched launch; any other callable is applied per image and stacked, as the reference does."""
+
+    def __init__(self, image_processor):
+        self.val_transform = image_processor
+
+    def preprocess_image(self, image):
+        if isinstance(image, list) and not isinstance(self.val_transform, DeviceImageProcessor):
+            return torch.stack([self.val_transform(img) for img in image])
+        return self.val_transform(image)

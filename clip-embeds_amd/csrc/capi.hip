@@ -153,6 +153,10 @@ struct ce_handle {
     bool timing = false;
     std::string timing_only;     // non-empty: only launches with this tag are bracketed
     float* cur_part = nullptr;   // GEMM split-K slabs of the tower whose launches are being issued
+    // LayerNorm folding of the vision blocks: enabled unless CE_LN_FOLD=0 /
+    // ce_set_ln_fold(h, 0); folded[name] = "<name>@fold{,_c,_d}" are current for weight `name`
+    bool ln_fold = true;
+    std::map<std::string, bool> folded;
     // text-tower training: caller-owned f32 master values and gradient slots per
     // trainable tensor (device pointers), saved activations of the last ce_text_forward_train
     std::map<std::string, std::pair<float*, float*>> bound;
@@ -339,6 +343,8 @@ struct TowerWs {
     int* rows;
     float* part;     // GEMM split-K partial tiles (ce::kGemmPartElems f32), per tower: the towers may
                      // run concurrently on two streams
+    float2* stats;        // LN folding: (mu, rstd) per row of the residual stream
+    float2* stats_part;   // LN folding: per-64-column-slab (mean, M2) from the residual GEMMs
 };
 
 size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
@@ -351,6 +357,8 @@ size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
     n += align256(B * D * 4);
     n += align256(B * 4);
     n += align256(ce::kGemmPartElems * 4);
+    n += align256(rows * 8);
+    n += align256(rows * (D / 64) * 8);
     return n;
 }
 
@@ -364,7 +372,9 @@ TowerWs carve(char* base, long rows, int D, int F, long extra_hid_elems, long B)
     w.hid = (bf16_t*)p; p += align256(std::max(rows * F, extra_hid_elems) * 2);
     w.pooled = (float*)p; p += align256(B * D * 4);
     w.rows = (int*)p; p += align256(B * 4);
-    w.part = (float*)p;
+    w.part = (float*)p; p += align256(ce::kGemmPartElems * 4);
+    w.stats = (float2*)p; p += align256(rows * 8);
+    w.stats_part = (float2*)p;
     return w;
 }
 
@@ -410,9 +420,17 @@ int ensure_tmp(ce_handle* h, size_t need) {
 
 // ---------------------------------------------------------------------------------------------
 // building blocks
+struct EpiArgs {
+    int epi = ce::EPI_PLAIN;
+    bf16_t* xb = nullptr;
+    float2* stats_part = nullptr;
+    const float2* fold_stats = nullptr;
+    const float* fold_c = nullptr;
+};
+
 int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
          int M, int N, int K, const float* bias, int act, const float* resid, void* out, bool out_bf16,
-         int grp = 0, int o_gs = 0, int o_go = 0, int r_gs = 0, int r_go = 0) {
+         int grp = 0, int o_gs = 0, int o_go = 0, int r_gs = 0, int r_go = 0, const EpiArgs& ea = EpiArgs()) {
     ce::GemmParams p{};
     p.A = A; p.lda = lda; p.W = Wt; p.ldw = K;
     p.M = M; p.N = N; p.K = K;
@@ -422,10 +440,11 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.grp = grp; p.o_gs = o_gs; p.o_go = o_go; p.r_gs = r_gs; p.r_go = r_go;
     p.part = h->cur_part;            // split-K tail slabs of the tower being run (null: no split)
     p.part_elems = h->cur_part ? ce::kGemmPartElems : 0;
+    p.xb = ea.xb; p.stats_part = ea.stats_part; p.fold_stats = ea.fold_stats; p.fold_c = ea.fold_c;
     const double flops = 2.0 * M * N * K;
     const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
-                         (resid ? (double)M * N * 4 : 0.0);
-    return timed(h, s, tag, flops, bytes, [&] { return ce::launch_gemm(p, act, out_bf16, s); });
+                         (resid ? (double)M * N * 4 : 0.0) + (ea.xb ? (double)M * N * 2 : 0.0);
+    return timed(h, s, tag, flops, bytes, [&] { return ce::launch_gemm(p, act, out_bf16, s, ea.epi); });
 }
 
 int layernorm(ce_handle* h, hipStream_t s, const char* tag, const float* in, void* out, bool out_bf16,
@@ -477,6 +496,68 @@ int check_launch(hipError_t e, const char* what) {
     return CE_OK;
 }
 
+// folded weights of one vision block (fold_linear); null when the fold is not current
+struct FoldBlk {
+    const bf16_t *wqkv, *wfc;
+    const float *cqkv, *dqkv, *cfc, *dfc;
+};
+
+bool fold_block(const ce_handle* h, const std::string& p, FoldBlk& f) {
+    const std::string q = p + "attn.in_proj_weight", m = p + "mlp.c_fc.weight";
+    auto ok = [&](const std::string& n) { auto it = h->folded.find(n); return it != h->folded.end() && it->second; };
+    if (!ok(q) || !ok(m)) return false;
+    f.wqkv = W<bf16_t>(h, q + "@fold"); f.cqkv = W(h, q + "@fold_c"); f.dqkv = W(h, q + "@fold_d");
+    f.wfc = W<bf16_t>(h, m + "@fold"); f.cfc = W(h, m + "@fold_c"); f.dfc = W(h, m + "@fold_d");
+    return f.wqkv && f.cqkv && f.dqkv && f.wfc && f.cfc && f.dfc;
+}
+
+// run_block with both pre-LNs folded into their GEMMs.  On entry w.xn = bf16(w.x) and w.stats =
+// (mu, rstd) of every row of w.x; the residual GEMMs re-establish both for the next block (the
+// last block of the tower skips that).
+int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, const FoldBlk& f, int B, int L,
+                     int D, int H, int F, bool last) {
+    const int M = B * L;
+    struct PartScope {
+        ce_handle* h;
+        ~PartScope() { h->cur_part = nullptr; }
+    } scope{h};
+    h->cur_part = w.part;
+    EpiArgs fold;
+    fold.epi = ce::EPI_LN_FOLD;
+    fold.fold_stats = w.stats;
+    EpiArgs st;
+    st.epi = ce::EPI_LN_STATS;
+    st.xb = w.xn;
+    st.stats_part = w.stats_part;
+    auto finalize = [&] {
+        return timed(h, s, "ln_stats_v", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
+                     [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s); });
+    };
+    fold.fold_c = f.cqkv;
+    CE_TRY(gemm(h, s, "gemm_qkv_v", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_, nullptr, w.qkv, true,
+                0, 0, 0, 0, 0, fold));
+    {
+        const double flops = 4.0 * B * H * (double)L * L * 64;
+        const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
+        CE_TRY(timed(h, s, "attn_v", flops, bytes,
+                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, false, true, s); }));
+    }
+    CE_TRY(gemm(h, s, "gemm_out_v", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, w.x, w.x, false,
+                0, 0, 0, 0, 0, st));
+    CE_TRY(finalize());
+    fold.fold_c = f.cfc;
+    CE_TRY(gemm(h, s, "gemm_fc_v", w.xn, D, f.wfc, M, F, D, f.dfc, act_code(h), nullptr, w.hid, true,
+                0, 0, 0, 0, 0, fold));
+    if (last) {
+        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, w.x, w.x, false));
+    } else {
+        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, w.x, w.x, false,
+                    0, 0, 0, 0, 0, st));
+        CE_TRY(finalize());
+    }
+    return CE_OK;
+}
+
 // Vision tower.  Leaves the final residual stream in w.x.  out_pooled may be null.
 int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, bool pix_bf16, int B,
                float* out_pooled, bool normalize) {
@@ -490,11 +571,29 @@ int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, b
                 ce::ACT_NONE_, W(h, "visual.positional_embedding"), w.x, false, P, Lv, 1, 0, 1));
     CE_TRY(check_launch(ce::launch_cls_rows(w.x, W(h, "visual.class_embedding"), W(h, "visual.positional_embedding"),
                                             B, Lv, D, s), "cls_rows"));
-    CE_TRY(layernorm(h, s, "ln_v", w.x, w.x, false, W(h, "visual.ln_pre.weight"), W(h, "visual.ln_pre.bias"),
-                     B * Lv, D));
+    // LN folding needs every block's fold current and D a multiple of 64 (the slab statistics)
+    std::vector<FoldBlk> folds(c.vision.layers);
+    bool use_fold = h->ln_fold && D % 64 == 0 && D / 64 <= 64;
+    for (int i = 0; use_fold && i < c.vision.layers; ++i)
+        use_fold = fold_block(h, "visual.transformer.resblocks." + std::to_string(i) + ".", folds[i]);
+    if (use_fold) {
+        // ln_pre in place, also emitting bf16(x) and the row statistics block 0's folded LN needs
+        ce::LNParams p{};
+        p.in = w.x; p.ldi = D; p.out = w.x; p.ldo = D;
+        p.w = W(h, "visual.ln_pre.weight"); p.b = W(h, "visual.ln_pre.bias"); p.rows = B * Lv; p.D = D;
+        p.xb = w.xn; p.stats = w.stats;
+        CE_TRY(timed(h, s, "ln_v", 0.0, (double)B * Lv * D * 10.0, [&] { return ce::launch_layernorm(p, false, s); }));
+    } else {
+        CE_TRY(layernorm(h, s, "ln_v", w.x, w.x, false, W(h, "visual.ln_pre.weight"), W(h, "visual.ln_pre.bias"),
+                         B * Lv, D));
+    }
     for (int i = 0; i < c.vision.layers; ++i) {
         const Blk k = block_ptrs(h, "visual.transformer.resblocks." + std::to_string(i) + ".");
-        CE_TRY(run_block(h, s, w, k, B, Lv, D, c.vision.heads, c.vision.mlp_width, false, true));
+        if (use_fold)
+            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, Lv, D, c.vision.heads, c.vision.mlp_width,
+                                    i + 1 == c.vision.layers));
+        else
+            CE_TRY(run_block(h, s, w, k, B, Lv, D, c.vision.heads, c.vision.mlp_width, false, true));
     }
     if (out_pooled) {
         CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, nullptr, (long)Lv * D, B, D,
@@ -817,6 +916,7 @@ int ce_create(const ce_config* cfg, int device, ce_handle** out) {
     if (device < 0 || device >= ndev) return fail(CE_ERR_INVALID, "ce_create: device %d out of range (%d)", device, ndev);
     DeviceGuard g(device);
     ce_handle* h = new ce_handle();
+    if (const char* e = getenv("CE_LN_FOLD")) h->ln_fold = atoi(e) != 0;
     h->cfg = *cfg;
     h->device = device;
     h->G = cfg->image_size / cfg->patch_size;
@@ -866,10 +966,92 @@ int ce_destroy(ce_handle* h) {
     return CE_OK;
 }
 
+namespace {
+
+int tensor_f32(const ce_tensor& t, size_t cnt, std::vector<float>& f) {
+    f.resize(cnt);
+    switch (t.dtype) {
+        case CE_F32: memcpy(f.data(), t.data, cnt * 4); return CE_OK;
+        case CE_BF16: {
+            const uint16_t* s = (const uint16_t*)t.data;
+            for (size_t j = 0; j < cnt; ++j) f[j] = host_bf2f(s[j]);
+            return CE_OK;
+        }
+        case CE_F16: {
+            const uint16_t* s = (const uint16_t*)t.data;
+            for (size_t j = 0; j < cnt; ++j) f[j] = host_h2f(s[j]);
+            return CE_OK;
+        }
+        default: return fail(CE_ERR_INVALID, "ce_load_weights: '%s' unsupported dtype %d", t.name, t.dtype);
+    }
+}
+
+int upload_named(ce_handle* h, const std::string& name, const void* src, size_t bytes) {
+    void*& dp = h->dptr[name];
+    if (!dp) {
+        if (hipMalloc(&dp, bytes) != hipSuccess) {
+            dp = nullptr;
+            h->dptr.erase(name);
+            (void)hipGetLastError();
+            return fail(CE_ERR_OOM, "ce_load_weights: cannot allocate '%s'", name.c_str());
+        }
+    }
+    HIP_TRY(hipMemcpy(dp, src, bytes, hipMemcpyHostToDevice));
+    return CE_OK;
+}
+
+// LayerNorm folding.  The pre-LN of a block feeds exactly one GEMM, so
+//   Linear(LN(x))_n = s_n * (sum_k W_nk (gamma_k (x_k - mu) rstd + beta_k) + b_n)
+//                   = rstd * (sum_k W'_nk x_k - mu * c_n) + d_n
+// with W'_nk = bf16(s_n gamma_k W_nk), c_n = sum_k W'_nk (of the rounded values, so the mean
+// cancels exactly against the bf16 x the GEMM sees) and d_n = s_n (b_n + sum_k beta_k W_nk);
+// s_n = kAttnQScale on the q rows of in_proj, else 1.  Only when all four source tensors come in
+// one call is the fold recomputed; a partial update of any of them invalidates it.
+int fold_linear(ce_handle* h, const ce_tensor* t, const std::map<std::string, int>& idx, const std::string& wn,
+                const std::string& bn, const std::string& gn, const std::string& en, bool qrows) {
+    auto find = [&](const std::string& k) { auto it = idx.find(k); return it == idx.end() ? -1 : it->second; };
+    const int iw = find(wn), ib = find(bn), ig = find(gn), ie = find(en);
+    if (iw < 0 && ib < 0 && ig < 0 && ie < 0) return CE_OK;
+    if (iw < 0 || ib < 0 || ig < 0 || ie < 0) {
+        h->folded[wn] = false;
+        return CE_OK;
+    }
+    const std::vector<int64_t>& shp = h->specs.at(wn).shape;
+    const size_t N = (size_t)shp[0], K = (size_t)shp[1];
+    std::vector<float> W, b, g, e;
+    CE_TRY(tensor_f32(t[iw], N * K, W));
+    CE_TRY(tensor_f32(t[ib], N, b));
+    CE_TRY(tensor_f32(t[ig], K, g));
+    CE_TRY(tensor_f32(t[ie], K, e));
+    std::vector<uint16_t> wf(N * K);
+    std::vector<float> c(N), d(N);
+    const size_t nq = qrows ? N / 3 : 0;
+    for (size_t n = 0; n < N; ++n) {
+        const float sn = n < nq ? ce::kAttnQScale : 1.f;
+        double cs = 0.0, ds = 0.0;
+        for (size_t k = 0; k < K; ++k) {
+            const uint16_t v = host_f2bf(sn * (g[k] * W[n * K + k]));
+            wf[n * K + k] = v;
+            cs += host_bf2f(v);
+            ds += (double)e[k] * W[n * K + k];
+        }
+        c[n] = (float)cs;
+        d[n] = (float)((double)sn * ((double)b[n] + ds));
+    }
+    CE_TRY(upload_named(h, wn + "@fold", wf.data(), wf.size() * 2));
+    CE_TRY(upload_named(h, wn + "@fold_c", c.data(), N * 4));
+    CE_TRY(upload_named(h, wn + "@fold_d", d.data(), N * 4));
+    h->folded[wn] = true;
+    return CE_OK;
+}
+
+}  // namespace
+
 int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) {
     if (!h || (n > 0 && !t)) return fail(CE_ERR_INVALID, "ce_load_weights: null argument");
     DeviceGuard g(h->device);
     std::vector<float> f;
+    std::map<std::string, int> idx;   // canonical name -> index in t, for the LN folds below
     for (int i = 0; i < n; ++i) {
         if (!t[i].name) return fail(CE_ERR_INVALID, "ce_load_weights: tensor %d has no name", i);
         const std::string name = canonical(h, t[i].name);
@@ -897,21 +1079,8 @@ int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) 
         if (!t[i].data) return fail(CE_ERR_INVALID, "ce_load_weights: '%s' has no data", t[i].name);
         size_t cnt = 1;
         for (auto v : sp.shape) cnt *= (size_t)v;
-        f.resize(cnt);
-        switch (t[i].dtype) {
-            case CE_F32: memcpy(f.data(), t[i].data, cnt * 4); break;
-            case CE_BF16: {
-                const uint16_t* s = (const uint16_t*)t[i].data;
-                for (size_t j = 0; j < cnt; ++j) f[j] = host_bf2f(s[j]);
-                break;
-            }
-            case CE_F16: {
-                const uint16_t* s = (const uint16_t*)t[i].data;
-                for (size_t j = 0; j < cnt; ++j) f[j] = host_h2f(s[j]);
-                break;
-            }
-            default: return fail(CE_ERR_INVALID, "ce_load_weights: '%s' unsupported dtype %d", t[i].name, t[i].dtype);
-        }
+        CE_TRY(tensor_f32(t[i], cnt, f));
+        idx[name] = i;
         // Fold the attention score scale log2(e)/sqrt(head_dim) into the q rows of in_proj (the
         // first third of weight and bias): the attention kernel then works in log2 units with no
         // per-score multiply (attention.hip).  The host-side state dict keeps the original values.
@@ -952,17 +1121,15 @@ int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) 
                 break;
             }
         }
-        void*& dp = h->dptr[name];
-        if (!dp) {
-            if (hipMalloc(&dp, bytes.size()) != hipSuccess) {
-                dp = nullptr;
-                h->dptr.erase(name);
-                (void)hipGetLastError();
-                return fail(CE_ERR_OOM, "ce_load_weights: cannot allocate '%s'", name.c_str());
-            }
-        }
-        HIP_TRY(hipMemcpy(dp, bytes.data(), bytes.size(), hipMemcpyHostToDevice));
+        CE_TRY(upload_named(h, name, bytes.data(), bytes.size()));
         h->loaded[name] = true;
+    }
+    for (int l = 0; l < h->cfg.vision.layers; ++l) {
+        const std::string P = "visual.transformer.resblocks." + std::to_string(l) + ".";
+        CE_TRY(fold_linear(h, t, idx, P + "attn.in_proj_weight", P + "attn.in_proj_bias", P + "ln_1.weight",
+                           P + "ln_1.bias", true));
+        CE_TRY(fold_linear(h, t, idx, P + "mlp.c_fc.weight", P + "mlp.c_fc.bias", P + "ln_2.weight",
+                           P + "ln_2.bias", false));
     }
     return CE_OK;
 }
@@ -1557,6 +1724,12 @@ int ce_kernel_gemm_bf16(void* stream, const void* A, const void* Wt, int M, int 
 
 int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
 int ce_set_gemm_splitk(int enable) { return ce::set_gemm_splitk(enable); }
+int ce_set_ln_fold(ce_handle* h, int enable, int* previous) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_set_ln_fold: null handle");
+    if (previous) *previous = h->ln_fold ? 1 : 0;
+    h->ln_fold = enable != 0;
+    return CE_OK;
+}
 
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal) {
     if (!qkv || !out) return fail(CE_ERR_INVALID, "ce_kernel_attention: null argument");

@@ -26,8 +26,21 @@ struct GemmParams {
     // (partial f32 tiles into `part`), summed in fixed order by a fixup kernel
     float* part = nullptr; long part_elems = 0;
     int tail = 0, split = 1;
+    // LayerNorm folded into the GEMMs around it (EPI_LN_STATS / EPI_LN_FOLD):
+    //   producer (residual GEMM, f32 out): also xb[m][n] = bf16(out) and, per 64-column slab,
+    //     stats_part[m][n/64] = (mean, sum of squared deviations) of the outputs
+    //   consumer: A = bf16(x) (un-normalised), W = bf16(gamma o W); out = act(rstd_m * (acc -
+    //     mu_m * fold_c[n]) + bias[n]) with fold_stats[m] = (mu, rstd) and bias = b + W beta
+    bf16_t* xb = nullptr;
+    float2* stats_part = nullptr;
+    const float2* fold_stats = nullptr;
+    const float* fold_c = nullptr;
 };
-hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s);
+enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2 };
+hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
+// (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
+// combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
+hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s);
 int set_gemm_schedule(int v);   // returns previous
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
 float* gemm_kernel_api_workspace(long* elems);   // per-device partial-tile buffer (kernel-level API)
@@ -55,6 +68,10 @@ struct LNParams {
     // optional de-interleaving RoPE between the two (pacl.py:147-181; cos/sin [P][D/2]).
     const float* w2; const float* b2;
     const float* rope_cos; const float* rope_sin; int rope_P;
+    // optional (f32-output single LN, e.g. ln_pre): bf16 copy of the output and its row (mu, rstd)
+    // for an EPI_LN_FOLD consumer
+    bf16_t* xb = nullptr;
+    float2* stats = nullptr;
 };
 hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s);
 

@@ -85,10 +85,38 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, int
                                              0x00020000);
 }
 
-template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING>
+// LN-folded consumer operands of one wave's 128 x 16*NJ output block: per-column c_n and per-row
+// (mu, rstd).  CE_FOLD_PREFETCH=1 loads them at kernel start instead of at the epilogue; measured
+// 8% slower on the c_fc shape (registers held across the main loop), so off.
+template <int NJ>
+struct FoldOps {
+    float4 c[NJ];
+    float2 st[8];
+    __device__ __forceinline__ void load(const GemmParams& p, int mbase, int nbase, int lane) {
+        const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) c[j] = *reinterpret_cast<const float4*>(p.fold_c + nbase + j * 16 + fq * 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = p.fold_stats[min(mbase + i * 16 + fr, p.M - 1)];
+    }
+};
+
+#ifndef CE_FOLD_PREFETCH
+#define CE_FOLD_PREFETCH 0
+#endif
+
+template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
 __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase,
-                                                   int nbase, int lane) {
+                                                   int nbase, int lane, const FoldOps<NJ>* pre = nullptr) {
     const int fr = lane & 15, fq = lane >> 4;
+    // LN-folded consumer: per-column c_n and per-row (mu, rstd), loaded before any store is issued
+    FoldOps<NJ> fo;
+    if constexpr (EPI == EPI_LN_FOLD) {
+        if (pre) fo = *pre;
+        else fo.load(p, mbase, nbase, lane);
+    }
+    const float4 (&foldc)[NJ] = fo.c;
+    const float2 (&fst)[8] = fo.st;
     // bias through a buffer descriptor: a null bias gets num_records 0 and reads zeros, with no branch
     const __amdgpu_buffer_rsrc_t bsrd = make_srd(p.bias ? (const void*)p.bias : (const void*)p.A, p.bias ? p.N * 4 : 0);
     float4 bias[NJ];
@@ -117,13 +145,16 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         for (int i = 0; i < RD - 1; ++i) load_resid(i, rbuf[i]);
     }
     uint2 pend[NJ];      // bf16 output: packed values of the even fragment row, awaiting its partner
+    uint2 pxb[NJ];       // EPI_LN_STATS: bf16 copy of the even fragment row (16-B stores as for pend)
+    float2 sta, stb;     // EPI_LN_STATS: (mean, M2) of fragment rows fq and fq + 4 (this lane stores them)
+    float lmean, lm2;    // EPI_LN_STATS: running (mean, M2) of this lane's values of the current row
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         if constexpr (HAS_RESID) {
             if (i + RD - 1 < 8) load_resid(i + RD - 1, rbuf[(i + RD - 1) % RD]);
         }
         const int m = mbase + i * 16 + fr;
-        if constexpr (CHECK_M && !OUT_BF16) {
+        if constexpr (CHECK_M && !OUT_BF16 && EPI != EPI_LN_STATS) {
             if (m >= p.M) continue;
         }
         const size_t obase = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + nbase + fq * 4;
@@ -131,7 +162,16 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         for (int j = 0; j < NJ; ++j) {
             if (j >= jmax) break;
             f32x4 v = acc[i][j];
-            v[0] += bias[j].x; v[1] += bias[j].y; v[2] += bias[j].z; v[3] += bias[j].w;
+            if constexpr (EPI == EPI_LN_FOLD) {
+                // LN(x) W^T + b = rstd (x~ W'^T - mu c) + (b + W beta), W' = gamma o W (weight upload)
+                const float mu = fst[i].x, rs = fst[i].y;
+                v[0] = fmaf(rs, fmaf(-mu, foldc[j].x, v[0]), bias[j].x);
+                v[1] = fmaf(rs, fmaf(-mu, foldc[j].y, v[1]), bias[j].y);
+                v[2] = fmaf(rs, fmaf(-mu, foldc[j].z, v[2]), bias[j].z);
+                v[3] = fmaf(rs, fmaf(-mu, foldc[j].w, v[3]), bias[j].w);
+            } else {
+                v[0] += bias[j].x; v[1] += bias[j].y; v[2] += bias[j].z; v[3] += bias[j].w;
+            }
             if constexpr (ACT == ACT_GELU) {
                 const f32x2 lo = gelu_pair(f32x2{v[0], v[1]}), hi = gelu_pair(f32x2{v[2], v[3]});
                 v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
@@ -168,10 +208,62 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                     }
                 }
             } else {
-                *reinterpret_cast<float4*>(static_cast<float*>(p.out) + obase + j * 16) =
-                    make_float4(v[0], v[1], v[2], v[3]);
+                // (the stats epilogue runs the past-the-end rows of the last M tile, with clamped
+                // residual rows, so that each even row still meets its odd partner below)
+                if (EPI != EPI_LN_STATS || !CHECK_M || m < p.M)
+                    *reinterpret_cast<float4*>(static_cast<float*>(p.out) + obase + j * 16) =
+                        make_float4(v[0], v[1], v[2], v[3]);
+                if constexpr (EPI == EPI_LN_STATS) {
+                    // Chan's pairwise update: the 4 values of block j join the lane's 4j earlier ones
+                    const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+                    const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
+                    const float q4 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
+                    if (j == 0) {
+                        lmean = m4;
+                        lm2 = q4;
+                    } else {
+                        const float dl = m4 - lmean;
+                        lmean = fmaf(dl, 1.0f / (j + 1), lmean);
+                        lm2 += fmaf(dl * dl, 4.0f * j / (j + 1), q4);
+                    }
+                    const uint2 o = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                    if ((i & 1) == 0) {
+                        pxb[j] = o;
+                    } else {
+                        const auto x = __builtin_amdgcn_permlane16_swap(pxb[j].x, o.x, false, false);
+                        const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
+                        const int mrow = (fq & 1) ? m : m - 16;
+                        const size_t ob = (size_t)mrow * p.ldo + nbase + (fq & ~1) * 4 + j * 16;
+                        if (!CHECK_M || mrow < p.M)
+                            *reinterpret_cast<uint4*>(p.xb + ob) = make_uint4(x[0], y[0], x[1], y[1]);
+                    }
+                }
             }
         }
+        if constexpr (EPI == EPI_LN_STATS) {
+            // (mean, M2) of this row's 64-column slab: 4 lanes (fq) of 4*NJ values each, combined
+            // with Chan's formula for equal counts
+            float sm = lmean;
+            sm += __shfl_xor(sm, 16, 64);
+            sm += __shfl_xor(sm, 32, 64);
+            const float mean = sm * 0.25f;
+            const float dl = lmean - mean;
+            float q = fmaf(dl * dl, 4.0f * NJ, lm2);
+            q += __shfl_xor(q, 16, 64);
+            q += __shfl_xor(q, 32, 64);
+            // every lane now holds the row's result: lane group fq keeps rows fq and fq + 4
+            if (fq == (i & 3)) {
+                if (i < 4) sta = make_float2(mean, q);
+                else stb = make_float2(mean, q);
+            }
+        }
+    }
+    if constexpr (EPI == EPI_LN_STATS) {
+        // stored after all other stores (no divergent store inside the loop to upset vmcnt counting)
+        const int ma = mbase + fq * 16 + fr, mb = ma + 64;
+        const size_t ns = p.N / 64;
+        if (!CHECK_M || ma < p.M) p.stats_part[(size_t)ma * ns + nbase / 64] = sta;
+        if (!CHECK_M || mb < p.M) p.stats_part[(size_t)mb * ns + nbase / 64] = stb;
     }
 }
 
@@ -181,14 +273,14 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
 // fragment row i+1 are issued before the stores of row i (two-deep register ring).  Column slabs
 // are whole (N % 64 == 0), so the only bounds check is on rows, and only in the last M tile: the
 // interior path has no divergent branch, which keeps hipcc's waitcnt counting exact.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int NJ = 4, int RING = CE_RESID_RING>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int NJ = 4, int RING = CE_RESID_RING, int EPI = EPI_PLAIN>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase, int nbase,
-                                              int lane) {
+                                              int lane, const FoldOps<NJ>* pre = nullptr) {
     if (nbase >= p.N) return;                                   // wave-uniform
     if (mbase + 128 <= p.M)
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false, NJ, RING>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, false, NJ, RING, EPI>(p, acc, mbase, nbase, lane, pre);
     else
-        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true, NJ, RING>(p, acc, mbase, nbase, lane);
+        gemm_epilogue_rows<ACT, HAS_RESID, OUT_BF16, true, NJ, RING, EPI>(p, acc, mbase, nbase, lane, pre);
 }
 
 
@@ -501,7 +593,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_persist(GemmParams p) {
 //          W rows of quadrant-col nh}, each double-buffered; phase p computes one 64x32
 //          quadrant of every wave's 128x64 output (16 MFMAs) and issues the LDS-DMA of one
 //          half-tile of K-tile t+1, so every load has ~3 phases to land; one barrier per phase.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED, int RING = CE_RESID_RING>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED, int RING = CE_RESID_RING, int EPI = EPI_PLAIN>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
 
@@ -538,6 +630,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int fq = lane >> 4;
     const int frag_off0 = fr * 128 + ((((0 * 4) + fq) ^ (fr >> 1)) << 4);
     const int frag_off1 = fr * 128 + ((((1 * 4) + fq) ^ (fr >> 1)) << 4);
+
+    FoldOps<4> fold;
+    constexpr bool PRE = EPI == EPI_LN_FOLD && CE_FOLD_PREFETCH;
+    if constexpr (PRE) {
+        if (slab < 0 && n0 + wn * 64 < p.N) fold.load(p, m0 + wm * 128, n0 + wn * 64, lane);
+    }
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -722,13 +820,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
                 *reinterpret_cast<f32x4*>(dst + (size_t)i * 16 * BN + j * 16) = acc[i][j];
         return;
     }
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, RING>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, RING, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane,
+                                                           PRE ? &fold : nullptr);
 }
 
 // Split-K tail fixup: sums the `split` partial slabs of each tail tile in fixed order (deterministic)
 // and applies the epilogue (bias, activation, residual, f32/bf16 store).  One thread per 4 columns
 // of one row; 64 blocks of 256 threads per tile.
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
 __global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
     const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
     const int t_main = tiles_m * tiles_n - p.tail;
@@ -742,8 +841,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
     const float* src = p.part + (size_t)r * p.split * (BM * BN) + (size_t)row * BN + c4;
     f32x4 v = *reinterpret_cast<const f32x4*>(src);
     for (int c = 1; c < p.split; ++c) v += *reinterpret_cast<const f32x4*>(src + (size_t)c * (BM * BN));
-    if (p.bias) {
-        const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
+    const float4 b = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (EPI == EPI_LN_FOLD) {
+        const float4 c = *reinterpret_cast<const float4*>(p.fold_c + n);
+        const float2 st = p.fold_stats[m];
+        v[0] = fmaf(st.y, fmaf(-st.x, c.x, v[0]), b.x);
+        v[1] = fmaf(st.y, fmaf(-st.x, c.y, v[1]), b.y);
+        v[2] = fmaf(st.y, fmaf(-st.x, c.z, v[2]), b.z);
+        v[3] = fmaf(st.y, fmaf(-st.x, c.w, v[3]), b.w);
+    } else {
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
     }
     if constexpr (ACT == ACT_GELU) {
@@ -762,6 +868,19 @@ __global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
         *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     else
         *reinterpret_cast<float4*>(static_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+    if constexpr (EPI == EPI_LN_STATS) {
+        // a row's 256 columns are one wave (64 threads x 4); a 64-column slab = 16 consecutive lanes
+        *reinterpret_cast<uint2*>(p.xb + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        float sm = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) sm += __shfl_xor(sm, o2, 64);
+        const float mean = sm * (1.0f / 64);
+        float q = (v[0] - mean) * (v[0] - mean) + (v[1] - mean) * (v[1] - mean) + (v[2] - mean) * (v[2] - mean) +
+                  (v[3] - mean) * (v[3] - mean);
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) q += __shfl_xor(q, o2, 64);
+        if ((c4 & 63) == 0) p.stats_part[(size_t)m * (p.N / 64) + n / 64] = make_float2(mean, q);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -964,6 +1083,22 @@ float* kernel_api_part() {
     return g_part[dev];
 }
 
+// LN-fold / LN-stats epilogues exist for the default schedule only
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
+hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
+    GemmParams p = p0;
+    p.gm = gemm_groupm();
+    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    p.tail = 0;
+    p.split = 1;
+    plan_tail(p, nwg);
+    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
+                       dim3(nwg - p.tail + p.tail * p.split), dim3(NTHREADS), 0, s, p);
+    if (p.tail > 0)
+        hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
@@ -1037,10 +1172,21 @@ int set_gemm_schedule(int v) {
     return prev;
 }
 
-hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s) {
+hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi) {
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
+    if (epi == EPI_LN_STATS) {
+        if (act != ACT_NONE || !res || out_bf16 || !p.xb || !p.stats_part) return hipErrorInvalidValue;
+        return launch_epi<ACT_NONE, true, false, EPI_LN_STATS>(p, s);
+    }
+    if (epi == EPI_LN_FOLD) {
+        if (res || !out_bf16 || !p.fold_c || !p.fold_stats || !p.bias) return hipErrorInvalidValue;
+        if (act == ACT_NONE) return launch_epi<ACT_NONE, false, true, EPI_LN_FOLD>(p, s);
+        if (act == ACT_GELU) return launch_epi<ACT_GELU, false, true, EPI_LN_FOLD>(p, s);
+        if (act == ACT_QGELU) return launch_epi<ACT_QGELU, false, true, EPI_LN_FOLD>(p, s);
+        return hipErrorInvalidValue;
+    }
 #define CE_GEMM_CASE(A_, R_, O_) \
     if (act == A_ && res == R_ && out_bf16 == O_) return launch_t<A_, R_, O_>(p, s);
     CE_GEMM_CASE(ACT_NONE, false, true)

@@ -50,7 +50,7 @@ __device__ __forceinline__ void ln_inplace(float4 (&v)[NC], int D, const float* 
 }
 
 // One wave per row; 4 rows per 256-thread block.  D = NC * 256.
-template <int NC, bool OUT_BF16, bool DOUBLE, bool ROPE>
+template <int NC, bool OUT_BF16, bool DOUBLE, bool ROPE, bool STATS = false>
 __global__ __launch_bounds__(256) void layernorm_k(LNParams p) {
     __shared__ float rbuf[ROPE ? 4 * NC * 256 : 1];
     const int lane = threadIdx.x & 63;
@@ -85,6 +85,25 @@ __global__ __launch_bounds__(256) void layernorm_k(LNParams p) {
         for (int c = 0; c < NC; ++c) v[c] = *reinterpret_cast<const float4*>(rb + c * 256 + lane * 4);
     }
     if constexpr (DOUBLE) ln_inplace<NC>(v, D, p.w2, p.b2, lane);
+    if constexpr (STATS) {
+        // the output row is the next block's residual stream: its bf16 copy and (mu, rstd) feed an
+        // LN-folded GEMM (EPI_LN_FOLD) in place of that block's LayerNorm launch
+        float sm = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) sm += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+        const float mean = wave_sum(sm) / (float)D;
+        float q = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            q += ((v[c].x - mean) * (v[c].x - mean) + (v[c].y - mean) * (v[c].y - mean)) +
+                 ((v[c].z - mean) * (v[c].z - mean) + (v[c].w - mean) * (v[c].w - mean));
+        const float rstd = rsqrtf(wave_sum(q) / (float)D + 1e-5f);
+        if (lane == 0) p.stats[orow] = make_float2(mean, rstd);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            *reinterpret_cast<uint2*>(p.xb + (size_t)orow * p.ldo + c * 256 + lane * 4) =
+                make_uint2(pack_bf2(v[c].x, v[c].y), pack_bf2(v[c].z, v[c].w));
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const int e = c * 256 + lane * 4;
@@ -105,6 +124,11 @@ hipError_t ln_dispatch_nc(const LNParams& p, bool out_bf16, hipStream_t s) {
     const bool dbl = p.w2 != nullptr;
     const bool rope = p.rope_cos != nullptr;
     if (rope && !dbl) return hipErrorInvalidValue;
+    if (p.stats || p.xb) {
+        if (!p.stats || !p.xb || out_bf16 || dbl || rope) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((layernorm_k<NC, false, false, false, true>), grid, dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     if (out_bf16) {
         if (rope) hipLaunchKernelGGL((layernorm_k<NC, true, true, true>), grid, dim3(256), 0, s, p);
         else if (dbl) hipLaunchKernelGGL((layernorm_k<NC, true, true, false>), grid, dim3(256), 0, s, p);
@@ -271,7 +295,48 @@ __global__ __launch_bounds__(256) void f32_to_bf16_k(bf16_t* out, const float* i
     if (i < n) out[i] = f2bf(in[i]);
 }
 
+// (mu, rstd) of a row from equal-count (64-column) slab statistics (mean_s, M2_s):
+// mu = mean of the means, M2 = sum M2_s + 64 sum (mean_s - mu)^2 (Chan et al.), var = M2 / (64 n)
+// 16 lanes per row, lane k reading slab k (k, k+16, ...): the row's partials are one coalesced
+// 128-B read for D = 1024; Chan's combine of equal-size (64-column) slabs
+__global__ __launch_bounds__(256) void ln_stats_finalize_k(float2* __restrict__ stats, const float2* __restrict__ part,
+                                                           int rows, int nslab) {
+    const int r = blockIdx.x * 16 + (threadIdx.x >> 4), k0 = threadIdx.x & 15;
+    const bool live = r < rows;
+    const float2* pr = part + (size_t)(live ? r : 0) * nslab;
+    float2 v[4];
+    float sm = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int k = k0 + 16 * t;
+        v[t] = (live && k < nslab) ? pr[k] : make_float2(0.f, 0.f);
+        sm += v[t].x;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+    const float mu = sm / (float)nslab;
+    float m2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (k0 + 16 * t < nslab) {
+            const float d = v[t].x - mu;
+            m2 += v[t].y + 64.0f * d * d;
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+    if (live && k0 == 0) stats[r] = make_float2(mu, rsqrtf(m2 / (64.0f * nslab) + 1e-5f));
+}
+
 }  // namespace
+
+hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    if (nslab <= 0 || nslab > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ln_stats_finalize_k, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, stats, part, rows,
+                       nslab);
+    return hipGetLastError();
+}
 
 hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s) {
     if (p.rows <= 0) return hipSuccess;

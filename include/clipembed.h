@@ -248,6 +248,13 @@ int ce_set_gemm_schedule(int schedule);
 /* Split-K tail of the GEMM (default on): when a grid's last round holds few tiles, those tiles are
  * computed as K-chunks summed by a fixup launch.  Returns the previous setting.  For A/B. */
 int ce_set_gemm_splitk(int enable);
+/* LayerNorm folding of the image tower (default on; env CE_LN_FOLD=0 turns it off at ce_create):
+ * ln_1/ln_2 of every visual block are folded into the in_proj/c_fc weights at ce_load_weights,
+ * and the residual GEMMs emit the row statistics, so no LayerNorm launch remains inside the
+ * blocks.  Needs each block's in_proj/c_fc weight+bias and ln_1/ln_2 loaded in
+ * one ce_load_weights call; otherwise the unfolded path runs.  *previous (may be null) gets the
+ * previous setting. */
+int ce_set_ln_fold(ce_handle* h, int enable, int* previous);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);
 /* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */

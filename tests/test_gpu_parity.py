@@ -130,6 +130,60 @@ def test_full_depth_retrieval_top1_vs_oracle():
     assert (got.argmax(1) == ref.argmax(1)).all() and (got.argmax(0) == ref.argmax(0)).all()
 
 
+def _ran_folded(m, fn):
+    """Run fn() with kernel timing on; True when the folded LayerNorm path ran (its stats launches)."""
+    e = m._engine
+    e.set_timing(True)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        names = {k["name"] for k in e.kernel_stats()}
+    finally:
+        e.set_timing(False)
+    return out, "ln_stats_v" in names
+
+
+def test_ln_fold_matches_unfolded():
+    """Image tower with ln_1/ln_2 folded into in_proj/c_fc (default) vs the LayerNorm path, at full
+    depth: pooled and token outputs within 2e-4 cosine of each other and both within 1e-3 of the
+    golden.  A partial reload of one LN weight invalidates that fold (the unfolded
+    path runs, with the new weight); a whole-block reload restores it."""
+    cfg = get_model_config("ViT-L-14-336")
+    m = make_model(cfg)
+    imgs = torch.from_numpy(W.synthetic_images(3, seed=99))
+    m.visual.output_tokens = True
+    try:
+        (pf, tf), folded = _ran_folded(m, lambda: m.encode_image(imgs))
+        assert folded
+        prev = m._engine.set_ln_fold(False)
+        assert prev
+        (pu, tu), folded = _ran_folded(m, lambda: m.encode_image(imgs))
+        assert not folded
+        m._engine.set_ln_fold(True)
+        assert cos_dist(pf.cpu().numpy(), pu.cpu().numpy()) < 2e-4
+        assert cos_dist(tf.cpu().numpy()[:, ROWS_V], tu.cpu().numpy()[:, ROWS_V]) < 2e-4
+        sd = W.synthetic_state_dict(cfg)
+        o = O.encode_image(sd, imgs.numpy(), cfg)
+        assert cos_dist(pf.cpu().numpy(), o) < COS_TOL
+        # partial reload: one LN weight alone -> fold of that block is stale -> unfolded path
+        k = "visual.transformer.resblocks.3.ln_2.weight"
+        w2 = torch.from_numpy(sd[k] * 1.5)
+        m.load_state_dict({k: w2})
+        (p2, _), folded = _ran_folded(m, lambda: m.encode_image(imgs))
+        assert not folded
+        sd2 = dict(sd)
+        sd2[k] = w2.numpy()
+        assert cos_dist(p2.cpu().numpy(), O.encode_image(sd2, imgs.numpy(), cfg)) < COS_TOL
+        # whole block reload refolds it
+        pfx = "visual.transformer.resblocks.3."
+        m.load_state_dict({n: torch.from_numpy(np.asarray(v)) for n, v in sd2.items() if n.startswith(pfx)})
+        (p3, _), folded = _ran_folded(m, lambda: m.encode_image(imgs))
+        assert folded
+        assert cos_dist(p3.cpu().numpy(), p2.cpu().numpy()) < 2e-4
+    finally:
+        m.visual.output_tokens = False
+
+
 @pytest.fixture(scope="module")
 def pacl_models():
     cfg = get_model_config("ViT-L-14-336").with_depth(2, 2)

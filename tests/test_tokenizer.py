@@ -77,3 +77,23 @@ def test_call_surface(tok):
     os.environ.setdefault("CLIPEMBED_BPE_PATH", _bpe())
     assert torch.equal(T.tokenize(["a photo of a cat"]), out)
     assert T.get_tokenizer("ViT-B-16").context_length == 77
+
+
+def test_prepare_data_text_half(monkeypatch):
+    """prepare_data / prepare_data_clip .preprocess_text (data/utils.py:54-55, 69-70) tokenize with
+    the ViT-L-14-336 tokenizer: same ids as the golden default-mode rows."""
+    import clipembed
+    monkeypatch.setenv("CLIPEMBED_BPE_PATH", _bpe())
+    calls = []
+
+    def proc(img):                     # a host-side image processor, applied per image and stacked
+        calls.append(img)
+        return torch.full((3, 4, 4), float(img))
+
+    pd = clipembed.prepare_data_clip(proc)
+    x = pd.preprocess_image([1, 2, 3])
+    assert x.shape == (3, 3, 4, 4) and calls == [1, 2, 3]
+    assert float(pd.preprocess_image(5)[0, 0, 0]) == 5.0
+    ids = pd.preprocess_text(TEXTS[:4])
+    ref = T.SimpleTokenizer(bpe_path=_bpe())(TEXTS[:4])
+    assert ids.dtype == torch.long and torch.equal(ids, ref)

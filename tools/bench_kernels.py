@@ -56,6 +56,7 @@ def main():
         # epilogue ablations: the vision shapes with a plain bf16 store (no GELU / residual / f32 out)
         "fc_v_plain": (Mv, 4096, 1024, 0, False, True), "out_v_plain": (Mv, 1024, 1024, 0, False, True),
         "proj_v_plain": (Mv, 1024, 4096, 0, False, True),
+        "out_v_f32": (Mv, 1024, 1024, 0, False, False), "proj_v_f32": (Mv, 1024, 4096, 0, False, False),
     }
     if args.only:
         keep = set(args.only.split(","))
@@ -82,6 +83,7 @@ def main():
     for rnd in range(args.rounds):
         for sched in args.scheds.split(","):   # "1", "1g4" (tile-order M-group 4), "1r3" (resid ring 3),
             # "1n" (split-K tail off)
+            # suffix "n": split-K tail off
             _lib.lib().ce_set_gemm_splitk(0 if sched.endswith("n") else 1)
             sc, _, rg = sched.rstrip("n").partition("r")
             sc, _, gm = sc.partition("g")
