@@ -146,8 +146,11 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
     }
     uint2 pend[NJ];      // bf16 output: packed values of the even fragment row, awaiting its partner
     uint2 pxb[NJ];       // EPI_LN_STATS: bf16 copy of the even fragment row (16-B stores as for pend)
-    float2 sta, stb;     // EPI_LN_STATS: (mean, M2) of fragment rows fq and fq + 4 (this lane stores them)
-    float lmean, lm2;    // EPI_LN_STATS: running (mean, M2) of this lane's values of the current row
+    // EPI_LN_STATS, per 64-column slab (NJ/4 of them): (mean, M2) of fragment rows fq and fq + 4
+    // (this lane stores them) and the running (mean, M2) of this lane's values of the current row
+    constexpr int NS = NJ / 4;
+    float2 sta[NS], stb[NS];
+    float lmean[NS], lm2[NS];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         if constexpr (HAS_RESID) {
@@ -218,13 +221,14 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                     const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
                     const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
                     const float q4 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
-                    if (j == 0) {
-                        lmean = m4;
-                        lm2 = q4;
+                    const int sl = j >> 2, jj = j & 3;
+                    if (jj == 0) {
+                        lmean[sl] = m4;
+                        lm2[sl] = q4;
                     } else {
-                        const float dl = m4 - lmean;
-                        lmean = fmaf(dl, 1.0f / (j + 1), lmean);
-                        lm2 += fmaf(dl * dl, 4.0f * j / (j + 1), q4);
+                        const float dl = m4 - lmean[sl];
+                        lmean[sl] = fmaf(dl, 1.0f / (jj + 1), lmean[sl]);
+                        lm2[sl] += fmaf(dl * dl, 4.0f * jj / (jj + 1), q4);
                     }
                     const uint2 o = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
                     if ((i & 1) == 0) {
@@ -243,18 +247,21 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         if constexpr (EPI == EPI_LN_STATS) {
             // (mean, M2) of this row's 64-column slab: 4 lanes (fq) of 4*NJ values each, combined
             // with Chan's formula for equal counts
-            float sm = lmean;
-            sm += __shfl_xor(sm, 16, 64);
-            sm += __shfl_xor(sm, 32, 64);
-            const float mean = sm * 0.25f;
-            const float dl = lmean - mean;
-            float q = fmaf(dl * dl, 4.0f * NJ, lm2);
-            q += __shfl_xor(q, 16, 64);
-            q += __shfl_xor(q, 32, 64);
-            // every lane now holds the row's result: lane group fq keeps rows fq and fq + 4
-            if (fq == (i & 3)) {
-                if (i < 4) sta = make_float2(mean, q);
-                else stb = make_float2(mean, q);
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl) {
+                float sm = lmean[sl];
+                sm += __shfl_xor(sm, 16, 64);
+                sm += __shfl_xor(sm, 32, 64);
+                const float mean = sm * 0.25f;
+                const float dl = lmean[sl] - mean;
+                float q = fmaf(dl * dl, 16.0f, lm2[sl]);
+                q += __shfl_xor(q, 16, 64);
+                q += __shfl_xor(q, 32, 64);
+                // every lane now holds the row's result: lane group fq keeps rows fq and fq + 4
+                if (fq == (i & 3)) {
+                    if (i < 4) sta[sl] = make_float2(mean, q);
+                    else stb[sl] = make_float2(mean, q);
+                }
             }
         }
     }
@@ -262,8 +269,11 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
         // stored after all other stores (no divergent store inside the loop to upset vmcnt counting)
         const int ma = mbase + fq * 16 + fr, mb = ma + 64;
         const size_t ns = p.N / 64;
-        if (!CHECK_M || ma < p.M) p.stats_part[(size_t)ma * ns + nbase / 64] = sta;
-        if (!CHECK_M || mb < p.M) p.stats_part[(size_t)mb * ns + nbase / 64] = stb;
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (!CHECK_M || ma < p.M) p.stats_part[(size_t)ma * ns + nbase / 64 + sl] = sta[sl];
+            if (!CHECK_M || mb < p.M) p.stats_part[(size_t)mb * ns + nbase / 64 + sl] = stb[sl];
+        }
     }
 }
 
@@ -998,6 +1008,298 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4(GemmParams p) {
     gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+// ------------------------------------------------------------------------------------------
+// SCHED 10 ("w4p"): 4 waves (one per SIMD), 128x128 per wave (acc[8][8] in AGPRs), BK = 64 with
+// two 64-KB LDS buffers and global prefetch two K-tiles deep.  All fragments of a K-tile live in
+// registers (two sets: k 0-31 and k 32-63), so a buffer is free as soon as the reads of its second
+// set have landed, long before the MFMAs finish with it; the DMA of K-tile t+2 then goes into the
+// buffer of K-tile t.  Per K-tile, 128 MFMAs in three interleaved blocks:
+//   B1: MFMA(set0, rows 0-3)  + 16 ds_read (set1 of t)          -> lgkmcnt(0), barrier
+//   B2: MFMA(set0, rows 4-7) + MFMA(set1, rows 0-3) + 16 DMA (t+2 -> this buffer)
+//                                                              -> vmcnt(16) (t+1 landed), barrier
+//   B3: MFMA(set1, rows 4-7)  + 16 ds_read (set0 of t+1, other buffer)
+// Interleaving by sched_group_barrier (MFMA/DS/VMEM classes); 2 barriers per K-tile.  LDS image as
+// SCHED 1 (128-B rows, chunk c of row r at c ^ ((r>>1)&7)).  Past-K DMAs are issued with an
+// out-of-range offset (no traffic) so every iteration is identical.
+template <int ACT, bool HAS_RESID, bool OUT_BF16>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_w4p(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int wgid = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int nk = p.K / BK;
+
+    // staging: instruction j of wave w moves rows j*32 + w*8 + (lane>>3), 16-B chunk lane&7 of the
+    // LDS row, fetched from source chunk (lane&7) ^ ((row>>1)&7)
+    const int srow = wave * 8 + (lane >> 3);
+    const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
+    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
+    const int jstrA = 32 * (int)p.lda * 2, jstrW = 32 * (int)p.ldw * 2;
+    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
+    const __amdgpu_buffer_rsrc_t srdW = make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, BN)) * (int)p.ldw * 2);
+    auto dma = [&](int kt, int buf, int j) {     // j 0..7: A, 8..15: W
+        const int kb = kt < nk ? kt * BK * 2 : 0x7ffff000;
+        char* base = smem + buf * STAGE_BYTES;
+        if (j < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + (j * 32 + wave * 8) * 128), 16,
+                                                     voffA + j * jstrA, kb, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + TILE_BYTES + ((j - 8) * 32 + wave * 8) * 128),
+                                                     16, voffW + (j - 8) * jstrW, kb, 0, 0);
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int fo0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
+    const int fo1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 128 * 128;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+    // prologue: K-tiles 0 and 1 in flight, set0 of K-tile 0
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(0, 0, j);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(1, 1, j);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    barrier();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        a0[q] = *reinterpret_cast<const bf16x8*>(smem + a_off + q * 16 * 128 + fo0);
+        b0[q] = *reinterpret_cast<const bf16x8*>(smem + w_off + q * 16 * 128 + fo0);
+    }
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        const char* sb = smem + buf * STAGE_BYTES;
+        const char* so = smem + (buf ^ 1) * STAGE_BYTES;
+        // ---- B1 ----
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
+            a1[q] = *reinterpret_cast<const bf16x8*>(sb + a_off + q * 16 * 128 + fo1);
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- B2 ----
+#pragma unroll
+        for (int i = 4; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dma(kt + 2, buf, j);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- B3 ----
+#pragma unroll
+        for (int i = 4; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            a0[q] = *reinterpret_cast<const bf16x8*>(so + a_off + q * 16 * 128 + fo0);
+            b0[q] = *reinterpret_cast<const bf16x8*>(so + w_off + q * 16 * 128 + fo0);
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 2);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// SCHED 11 ("w4p persistent"): SCHED 10's main loop as one continuous K-tile stream over the
+// tiles a workgroup owns (grid = one workgroup per CU; tile r*grid + xcd_remap(b) in round r).
+// The DMA two K-tiles ahead runs into the next tile's first K-tiles, so the next tile's
+// operands are in flight while this tile's epilogue runs and there is no per-tile prologue.
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int grid = gridDim.x;
+    const int slot = xcd_remap(blockIdx.x, grid);
+    const int nk = p.K / BK;
+    const int my_tiles = slot < nwg ? (nwg - 1 - slot) / grid + 1 : 0;
+    const int nsteps = my_tiles * nk;
+
+    const int srow = wave * 8 + (lane >> 3);
+    const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
+    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
+    const int jstrA = 32 * (int)p.lda * 2, jstrW = 32 * (int)p.ldw * 2;
+    // DMA stream state: K-tile `dk` of this workgroup's tile number `dt` (0-based), descriptors
+    // for that tile; advanced once per K-tile
+    int dt = 0, dk = 0;
+    __amdgpu_buffer_rsrc_t srdA, srdW;
+    auto set_srd = [&](int t) {
+        int tm, tn;
+        tile_of(min(slot + t * grid, nwg - 1), tiles_m, tiles_n, p.gm, tm, tn);
+        const int mm = tm * BM, nn = tn * BN;
+        srdA = make_srd(p.A + (size_t)mm * p.lda, max(0, min(p.M - mm, BM)) * (int)p.lda * 2);
+        srdW = make_srd(p.W + (size_t)nn * p.ldw, max(0, min(p.N - nn, BN)) * (int)p.ldw * 2);
+    };
+    set_srd(0);
+    auto dma = [&](int buf, int j, bool live) {
+        const int kb = live ? dk * BK * 2 : 0x7ffff000;
+        char* base = smem + buf * STAGE_BYTES;
+        if (j < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + (j * 32 + wave * 8) * 128), 16,
+                                                     voffA + j * jstrA, kb, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + TILE_BYTES + ((j - 8) * 32 + wave * 8) * 128),
+                                                     16, voffW + (j - 8) * jstrW, kb, 0, 0);
+    };
+    auto advance = [&] {
+        if (++dk == nk) {
+            dk = 0;
+            ++dt;
+            set_srd(dt);
+        }
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int fo0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
+    const int fo1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 128 * 128;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+    // prologue: steps 0 and 1 in flight, set0 of step 0
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(0, j, 0 < nsteps);
+    advance();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(1, j, 1 < nsteps);
+    advance();
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    barrier();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        a0[q] = *reinterpret_cast<const bf16x8*>(smem + a_off + q * 16 * 128 + fo0);
+        b0[q] = *reinterpret_cast<const bf16x8*>(smem + w_off + q * 16 * 128 + fo0);
+    }
+
+    // MFMAs as inline asm with the accumulator pinned in AGPRs ("+a"): with the builtin, hipcc
+    // shuffles accumulators between AGPRs and VGPRs in this loop.  A volatile asm is also a
+    // barrier for memory instructions in the machine scheduler, so the ds_reads and DMAs below
+    // stay exactly where the source interleaves them; hipcc still inserts the lgkmcnt waits for
+    // the fragments each MFMA reads.
+#define CE_MFMA_AGPR(ACC, BV, AV) \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
+    int g = 0;
+    for (int t = 0; t < my_tiles; ++t) {
+        for (int kt = 0; kt < nk; ++kt, ++g) {
+            const int buf = g & 1;
+            const char* sb = smem + buf * STAGE_BYTES;
+            const char* so = smem + (buf ^ 1) * STAGE_BYTES;
+            // ---- B1: MFMA(set0, rows 0-3), set1 of this K-tile read under it (one per 2 MFMAs) ----
+#pragma unroll
+            for (int s2 = 0; s2 < 32; ++s2) {
+                const int i = s2 >> 3, j = s2 & 7;
+                CE_MFMA_AGPR(acc[i][j], b0[j], a0[i]);
+                if (s2 & 1) {
+                    const int q = s2 >> 1;      // 0..15: b1[0..7], a1[0..7]
+                    if (q < 8) b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
+                    else a1[q - 8] = *reinterpret_cast<const bf16x8*>(sb + a_off + (q - 8) * 16 * 128 + fo1);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier();
+            // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); DMA of step g+2 (one per 4) ----
+            const bool live = g + 2 < nsteps;
+#pragma unroll
+            for (int s2 = 0; s2 < 64; ++s2) {
+                const int i = (s2 >> 3) & 3, j = s2 & 7;
+                if (s2 < 32) CE_MFMA_AGPR(acc[4 + i][j], b0[j], a0[4 + i]);
+                else CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
+                if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
+            }
+            advance();
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            barrier();
+            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it (the last K-tile's
+            // reads fetch the next tile's K-tile 0) ----
+#pragma unroll
+            for (int s2 = 0; s2 < 32; ++s2) {
+                const int i = s2 >> 3, j = s2 & 7;
+                CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+                if (s2 & 1) {
+                    const int q = s2 >> 1;      // a0[0], b0[0..7], a0[1..7]
+                    if (q == 0) a0[0] = *reinterpret_cast<const bf16x8*>(so + a_off + fo0);
+                    else if (q < 9) b0[q - 1] = *reinterpret_cast<const bf16x8*>(so + w_off + (q - 1) * 16 * 128 + fo0);
+                    else a0[q - 8] = *reinterpret_cast<const bf16x8*>(so + a_off + (q - 8) * 16 * 128 + fo0);
+                }
+            }
+        }
+        int tm, tn;
+        tile_of(slot + t * grid, tiles_m, tiles_n, p.gm, tm, tn);
+        gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8, CE_RESID_RING, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128,
+                                                                     lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#undef CE_MFMA_AGPR
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 int g_sched = -1;
 int g_ring = CE_RESID_RING;     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
 int gemm_sched() {
@@ -1005,7 +1307,7 @@ int gemm_sched() {
         const char* e = getenv("CE_GEMM_SCHED");
         g_sched = e ? atoi(e) : 1;
         if (!(g_sched == 0 || g_sched == 1 || g_sched == 2 || g_sched == 3 || g_sched == 4 || g_sched == 6 ||
-              g_sched == 7 || g_sched == 9))
+              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11))
             g_sched = 1;
     }
     return g_sched;
@@ -1083,10 +1385,42 @@ float* kernel_api_part() {
     return g_part[dev];
 }
 
-// LN-fold / LN-stats epilogues exist for the default schedule only
+// SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
+int w4pp_grid(int nwg) {
+    int grid = (num_cus() / 8) * 8;
+    const int need = ((nwg + 7) / 8) * 8;
+    return grid < need ? grid : need;
+}
+
+// Optional shape policy (CE_GEMM_AUTO=1; off by default): SCHED 11 for the plain QKV shape and
+// K >= 2048 residual GEMMs, where it wins as a bare GEMM (QKV +6 %, tools/bench_kernels.py).  In
+// the model those GEMMs carry the LN-fold / LN-stats epilogues, which cost more with one wave per
+// SIMD than SCHED 1's two (bench: QKV 23.5 vs 22.3 ms/step, c_proj 31.5 vs 28.2), so SCHED 1 stays
+// the default.  Only for grids of >= 4 tiles per CU.
+bool auto_w4pp(const GemmParams& p, int act, bool resid) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("CE_GEMM_AUTO");
+        on = e ? atoi(e) != 0 : 0;
+    }
+    if (!on || gemm_sched() != 1) return false;
+    // enough tiles that the persistent grid's last-round imbalance stays small (small grids keep
+    // SCHED 1 and its split-K tail)
+    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    if (nwg < 4 * num_cus()) return false;
+    return (act == ACT_NONE && !resid) || (resid && p.K >= 2048);
+}
+
+// LN-fold / LN-stats epilogues exist for SCHED 1 and SCHED 11
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
+    if (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID)) {
+        p.gm = gemm_groupm();
+        const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     p.tail = 0;
@@ -1104,7 +1438,7 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
     p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    const int sc = gemm_sched();
+    const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : gemm_sched();
     p.tail = 0;
     p.split = 1;
     if (sc == 1) {
@@ -1125,7 +1459,11 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         const int need = ((nwg + 7) / 8) * 8;
         grid = grid < need ? grid : need;
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
-    } else if (sc == 2)
+    } else if (sc == 11) {
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+    } else if (sc == 10)
+        hipLaunchKernelGGL((gemm_bf16_w4p<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
+    else if (sc == 2)
         hipLaunchKernelGGL((gemm_bf16_w4<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
     else if (sc == 0)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
@@ -1167,7 +1505,7 @@ int set_gemm_schedule(int v) {
     const int prev = gemm_sched() | (gemm_groupm() << 8);
     const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff;
     if (ring >= 2 && ring <= 5) g_ring = ring;
-    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9) ? sc : 1;
+    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 || sc == 11) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }
