@@ -101,6 +101,10 @@ struct FoldOps {
     }
 };
 
+#ifndef CE_W4_EPI_HALVES
+#define CE_W4_EPI_HALVES 1
+#endif
+
 #ifndef CE_FOLD_PREFETCH
 #define CE_FOLD_PREFETCH 0
 #endif
@@ -1289,8 +1293,23 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         }
         int tm, tn;
         tile_of(slot + t * grid, tiles_m, tiles_n, p.gm, tm, tn);
+#if CE_W4_EPI_HALVES
+        // the 128-column quadrant as two 64-column epilogues: the NJ = 4 path (4-deep residual
+        // ring, a quarter of the live epilogue registers)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f32x4 q[8][4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[i][j] = acc[i][h * 4 + j];
+            gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>(
+                p, q, tm * BM + wm * 128, tn * BN + wn * 128 + h * 64, lane);
+        }
+#else
         gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8, CE_RESID_RING, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128,
                                                                      lane);
+#endif
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1392,23 +1411,25 @@ int w4pp_grid(int nwg) {
     return grid < need ? grid : need;
 }
 
-// Optional shape policy (CE_GEMM_AUTO=1; off by default): SCHED 11 for the plain QKV shape and
-// K >= 2048 residual GEMMs, where it wins as a bare GEMM (QKV +6 %, tools/bench_kernels.py).  In
-// the model those GEMMs carry the LN-fold / LN-stats epilogues, which cost more with one wave per
-// SIMD than SCHED 1's two (bench: QKV 23.5 vs 22.3 ms/step, c_proj 31.5 vs 28.2), so SCHED 1 stays
-// the default.  Only for grids of >= 4 tiles per CU.
+// Shape policy of the default schedule (CE_GEMM_AUTO, default 1): SCHED 11 for large grids with
+// no activation and no residual — the vision QKV GEMM, plain or LN-folded (in-model 20.3 vs 23.1
+// ms/step).  Epilogues with GELU or a residual stay on SCHED 1: one wave per SIMD pays them
+// serially (c_fc + fold + GELU 35.9 vs 34.4, c_proj + stats 30.0 vs 29.3, out-proj 14.0 vs 12.8;
+// profiles/r01_gemm_w4p_sched10_11.log).  CE_GEMM_AUTO=0 pins SCHED 1, =2 sends every large
+// grid to SCHED 11.  Only for grids of >= 4 tiles per CU.
 bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     static int on = -1;
     if (on < 0) {
         const char* e = getenv("CE_GEMM_AUTO");
-        on = e ? atoi(e) != 0 : 0;
+        on = e ? atoi(e) : 1;
     }
     if (!on || gemm_sched() != 1) return false;
     // enough tiles that the persistent grid's last-round imbalance stays small (small grids keep
     // SCHED 1 and its split-K tail)
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (nwg < 4 * num_cus()) return false;
-    return (act == ACT_NONE && !resid) || (resid && p.K >= 2048);
+    if (on == 2) return true;
+    return act == ACT_NONE && !resid;
 }
 
 // LN-fold / LN-stats epilogues exist for SCHED 1 and SCHED 11
