@@ -1429,6 +1429,7 @@ bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     if (nwg < 4 * num_cus()) return false;
     if (on == 2) return true;
+    if (on == 3) return !resid;
     return act == ACT_NONE && !resid;
 }
 
