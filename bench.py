@@ -1,21 +1,37 @@
-"""Throughput benchmark of the CLIP ViT-L/14-336 embedding path (BASELINE.json configs[1]):
-encode_image + encode_text of a synthetic batch (336x336 images, 77-token captions) per GPU,
-L2-normalised, then (N > 1) an RCCL all-gather of both embedding sets and the local contrastive
-logits [B, N*B] in both directions — the data-parallel step of loss.py:137-164 with local_loss.
+"""Throughput benchmark of the CLIP ViT-L/14-336 embedding path, one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload clip|pacl|negclip|sparc] [--batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+`--gpus N > 1` without a launcher re-launches this script under torch.distributed.run as a child
+process (before any GPU call) and exits with its status; it never silently runs one rank.
+
+Workloads (BASELINE.json configs; a "step" is one pass of the hot path over one synthetic batch):
+  clip     (default, configs[1], the headline metric) encode_image + encode_text of B = 256 pairs per
+           GPU, L2-normalised; N > 1: RCCL all-gather of both embedding sets and the local
+           contrastive logits [B, N*B] both ways (loss.py:137-164, local_loss).
+  pacl     (configs[2]) PACL forward of B = 512 pairs per GPU (open_clip_pacl.forward, pacl.py:135-145:
+           text tower + head, vision tower + patch head, fused patch alignment/pooling) + the PACL
+           ClipLoss (pacl.py:489-514; N > 1: all-gathered features, local logits).
+  negclip  (configs[3]) NegCLIP training step, locked image tower: 1024 pairs + 512 hard-negative
+           captions per GPU, text tower backward, RCCL all-reduce of text gradients, AdamW.
+  sparc    (configs[4]) SPARC with precomputed text-token embeddings [B,77,768] + mask: image
+           tower + patch head, patch x token similarity / alignment (pacl.py:455-478) and SparcLoss
+           (pacl.py:516-584; N > 1: global term over all-gathered means) for B = 256 per GPU.
 
 Prints ONE JSON line (rank 0).  value = image-text pairs/s over all ranks (weak scaling: B pairs
 per GPU per step), inputs resident in HBM before the timed region.  `roofline` reports the
-dominant kernel (by total time in an untimed profile pass) measured with HIP events on its stream
-over the timed steps (only its launches carry events there);
-`cpu_baseline` times the f32 CPU oracle (oracle/clip_oracle.py, a restatement of the reference's
-PyTorch CPU forward) on a bounded sample on this host.
+dominant kernel (by total time in an untimed profile pass), measured with HIP events on its stream
+over the timed steps (only its launches carry events there); for pacl it also carries the pooling
+kernel's HBM rate.  `cpu_baseline` times the reference's CPU forward (oracle/clip_torch_cpu.py: the
+reference's own ATen calls, f32) on this host at batch 8, median of 3, at the host's core share
+and at 8 threads.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,32 +47,73 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0          # HBM3E spec
 FLOPS_PER_PAIR = 395.22e9      # open_clip/docs/model_profile.csv:65 (381.92 image + 13.30 text GFLOP)
+IMAGE_FLOPS = 381.92e9
+TEXT_FLOPS = 13.30e9
+PACL_HEAD_FLOPS = 2.49e9       # PACL patch head per image (+ the pooling, counted below)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sd, cfg, n_pairs):
-    """Time the f32 CPU oracle (the reference's algorithm restated in NumPy) on n_pairs pairs."""
-    from oracle import clip_oracle as O
-    from clipembed import weights as W
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(nproc):
+    """Run this script under torch.distributed.run with nproc ranks (a child process; no exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching:", " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+# ----------------------------------------------------------------------------------- CPU baseline
+def host_cores():
+    for k in ("OMP_NUM_THREADS",):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return int(v)
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = os.cpu_count() or 1
-    imgs = W.synthetic_images(n_pairs, seed=5000)
-    caps = W.synthetic_captions(n_pairs, seed=6000)
-    O.encode_text(sd, caps[:1], cfg)          # warm-up (BLAS init)
-    t0 = time.perf_counter()
-    fi = O.encode_image(sd, imgs, cfg, normalize=True)
-    ft = O.encode_text(sd, caps, cfg, normalize=True)
-    O.get_logits(fi, ft, 100.0)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_pairs / dt, 4), "unit": "pairs/s", "cores": int(threads), "kind": "port",
-            "sample": f"{n_pairs} image-text pairs, full-depth ViT-L/14-336 f32 NumPy oracle "
-                      f"(encode_image + encode_text + logits), {dt:.1f} s"}
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(sd, cfg, batch=8, reps=3):
+    """The reference's f32 CPU forward (encode_image + encode_text + logits) at `batch` pairs, median
+    of `reps`, at the host core share and at 8 threads."""
+    from oracle.clip_torch_cpu import TorchCLIP
+    from clipembed import weights as W
+    m = TorchCLIP(sd, cfg)
+    imgs = torch.from_numpy(W.synthetic_images(batch, seed=5000))
+    caps = torch.from_numpy(W.synthetic_captions(batch, seed=6000))
+    prev = torch.get_num_threads()
+    res = {}
+    cores = host_cores()
+    for n in sorted({cores, 8}, reverse=True):
+        torch.set_num_threads(n)
+        m.encode_image(imgs[:1])                 # warm-up (thread pool, allocator)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fi = m.encode_image(imgs, normalize=True)
+            ft = m.encode_text(caps, normalize=True)
+            m.get_logits(fi, ft, 100.0)
+            ts.append(time.perf_counter() - t0)
+        res[n] = float(np.median(ts))
+    torch.set_num_threads(prev)
+    out = {"value": round(batch / res[cores], 4), "unit": "pairs/s", "cores": cores, "kind": "port",
+           "sample": f"{batch} image-text pairs per run, median of {reps}: full-depth ViT-L/14-336 f32 torch CPU "
+                     f"forward with the reference's ATen calls (oracle/clip_torch_cpu.py), encode_image + "
+                     f"encode_text + logits; {res[cores]:.2f} s at {cores} threads"}
+    if 8 in res:
+        out["value_8_threads"] = round(batch / res[8], 4)
+    return out
 
 
 def load_traffic(tag):
@@ -70,63 +127,25 @@ def load_traffic(tag):
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="image-text pairs per GPU per step")
-    ap.add_argument("--cpu-pairs", type=int, default=8, help="pairs in the bounded CPU-baseline sample (~10 s)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
-    ap.add_argument("--text-stream", action="store_true", help="run the text tower on a second stream")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-
+# ----------------------------------------------------------------------------------- workloads
+def build_clip(args, dev, rank, world):
     import clipembed
-    from clipembed import weights as W
+    from clipembed import _lib, weights as W
     from clipembed.loss import all_gather_cat
-
     cfg = clipembed.get_model_config("ViT-L-14-336")
-    t0 = time.time()
     sd = W.synthetic_state_dict(cfg)
     model = clipembed.CLIP(cfg)
     model.load_state_dict(sd)
     model.to(dev)
-    B = args.batch
-    model.engine.h  # noqa: B018
-    from clipembed import _lib
+    B = args.batch or 256
     _lib.call("ce_reserve", model.engine.h, B, B)
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
     scale = float(model.logit_scale.detach().exp())
-    log(f"[rank {rank}] setup {time.time() - t0:.1f}s, batch {B}/GPU, world {world}")
-
-    side = torch.cuda.Stream(dev)
-    main_stream = torch.cuda.current_stream(dev)
 
     def step():
-        if args.text_stream:
-            # the text tower (its own workspace in the engine) on a second stream, overlapping the
-            # vision tower's tile tails and row kernels
-            side.wait_stream(main_stream)
-            with torch.cuda.stream(side):
-                ft = model.encode_text(caps, normalize=True)
-            fi = model.encode_image(imgs, normalize=True)
-            main_stream.wait_stream(side)
-            ft.record_stream(main_stream)
-        else:
-            fi = model.encode_image(imgs, normalize=True)
-            ft = model.encode_text(caps, normalize=True)
+        fi = model.encode_image(imgs, normalize=True)
+        ft = model.encode_text(caps, normalize=True)
         if world > 1:
             ai = all_gather_cat(fi, world)          # RCCL all-gather over xGMI
             at = all_gather_cat(ft, world)
@@ -136,6 +155,154 @@ def main():
             li, lt = model.logits(fi, ft, scale)
         return li, lt
 
+    cfgd = {"workload": "CLIP ViT-L/14-336 encode_image + encode_text + normalise + contrastive logits "
+                        "(BASELINE configs[1]: batch 256/GPU bf16)",
+            "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
+            "parallelism": f"dp{world}",
+            "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none"}
+    return dict(engine=model.engine, step=step, pairs=B, flops_per_pair=FLOPS_PER_PAIR, sd=sd, cfg=cfg,
+                metric="image-text pairs/sec ViT-L/14-336", config=cfgd)
+
+
+def build_pacl(args, dev, rank, world):
+    import clipembed
+    from clipembed import _lib, weights as W
+    from clipembed.loss import all_gather_cat
+    from clipembed.pacl import ClipLoss, open_clip_pacl, open_clip_pacl_rope_after
+    cfg = clipembed.get_model_config("ViT-L-14-336")
+    sd = W.synthetic_state_dict(cfg)
+    cls = open_clip_pacl_rope_after if args.pacl_mode == "sigmoid_rope_after" else open_clip_pacl
+    mod = cls(cfg=cfg, clip_state_dict=sd)
+    mod.init_synthetic_heads()
+    mod.to(dev)
+    B = args.batch or 512
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
+    caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
+    loss = ClipLoss(0.1, engine=mod.engine)        # train_pacl.py: temperature 0.1
+    labels = torch.arange(B, device=dev) + B * rank
+
+    def step():
+        oi, ot = mod(imgs, caps)
+        if world > 1:
+            ai, at = all_gather_cat(oi, world), all_gather_cat(ot, world)
+            li = mod.clip_model.logits(oi, at, loss.logit_scale, with_text_logits=False)[0]
+            lt = mod.clip_model.logits(ot, ai, loss.logit_scale, with_text_logits=False)[0]
+            return (loss._ce(mod.engine, li, labels) + loss._ce(mod.engine, lt, labels)) / 2
+        return loss(oi, ot)
+
+    pool_flops = 2.0 * 576 * 768 * (2 if cls.weight_mode else 1)
+    cfgd = {"workload": f"PACL patch-token forward ({cls.__name__}) + patch alignment/pooling + PACL ClipLoss "
+                        "(BASELINE configs[2]: batch 512/GPU bf16)",
+            "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
+            "parallelism": f"dp{world}", "pacl_mode": args.pacl_mode,
+            "exchange": "RCCL all_gather of pooled embeddings" if world > 1 else "none"}
+    return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
+                flops_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops,
+                metric="PACL image-text pairs/sec ViT-L/14-336", config=cfgd, hbm_kernel="pacl_pool")
+
+
+def build_negclip(args, dev, rank, world):
+    import clipembed
+    from clipembed import weights as W
+    cfg = clipembed.get_model_config("ViT-L-14-336")
+    sd = W.synthetic_state_dict(cfg)
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(sd)
+    m.to(dev)
+    B = args.batch or 1024
+    K = args.hard if args.hard is not None else B // 2
+    tr = clipembed.TextTowerTrainer(m, lr=5e-6, usehardtext=K > 0, rank=rank, world_size=world)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
+    caps = torch.from_numpy(W.synthetic_captions(B + K, seed=2000 + rank)).to(dev)
+
+    def step():
+        loss = tr.compute_grads(imgs, caps)
+        tr.apply_update()
+        return loss
+
+    # image forward + text forward/backward (x3) over B + K captions
+    flops = IMAGE_FLOPS + 3.0 * TEXT_FLOPS * (B + K) / B
+    cfgd = {"workload": "open_clip NegCLIP training step, locked image tower, text tower AdamW "
+                        "(BASELINE configs[3]: 1024 pairs + hard negatives per GPU, local loss, gather with grad)",
+            "batch_per_gpu": B, "hard_negatives_per_gpu": K, "global_batch": world * B, "parallelism": f"dp{world}",
+            "exchange": ("RCCL all_gather of embeddings + sizes, reduce_scatter of their gradients, "
+                         "all_reduce of text gradients") if world > 1 else "none"}
+    return dict(engine=m.engine, step=step, pairs=B, flops_per_pair=flops, sd=sd, cfg=cfg,
+                metric="NegCLIP training image-text pairs/sec ViT-L/14-336", config=cfgd)
+
+
+def build_sparc(args, dev, rank, world):
+    import clipembed
+    from clipembed import _lib, weights as W
+    from clipembed.loss import all_gather_cat
+    from clipembed.pacl import SparcLoss, sparc, sparc_rope
+    cfg = clipembed.get_model_config("ViT-L-14-336")
+    sd = W.synthetic_state_dict(cfg)
+    cls = sparc_rope if args.sparc_rope else sparc
+    mod = cls(sigma=1.0 / 576, cfg=cfg, clip_state_dict=sd)
+    mod.init_synthetic_heads()
+    mod.to(dev)
+    B, T, P, D = args.batch or 256, 77, 576, 768
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
+    # precomputed text-token embeddings (the train_sparc.py "LLM embeddings" input) + EOT mask
+    g = torch.Generator(device="cpu").manual_seed(3000 + rank)
+    l_tok = (torch.randn(B, T, D, generator=g) * 0.5).to(dev)
+    eot = torch.randint(6, 42, (B,), generator=g)
+    mask = (torch.arange(T).expand(B, -1) <= eot[:, None]).float().to(dev)
+    loss_fn = SparcLoss(0.07, engine=mod.engine)
+
+    def step():
+        v = mod.forward_visual(imgs)
+        gr, ln = mod.align(v, l_tok)
+        return loss_fn(v, ln, gr, mask)
+
+    sim_flops = 2.0 * T * P * D
+    cfgd = {"workload": f"SPARC ({cls.__name__}) image tower + patch head, patch x token similarity / alignment, "
+                        "SparcLoss with precomputed text-token embeddings (BASELINE configs[4]: batch 256/GPU)",
+            "batch_per_gpu": B, "global_batch": world * B, "tokens": T, "patches": P, "dim": D,
+            "parallelism": f"dp{world}", "exchange": "none (per-GPU SparcLoss)"}
+    return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
+                flops_per_pair=IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D,
+                metric="SPARC image-text pairs/sec ViT-L/14-336", config=cfgd)
+
+
+BUILDERS = {"clip": build_clip, "pacl": build_pacl, "negclip": build_negclip, "sparc": build_sparc}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(BUILDERS), default="clip")
+    ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step (0 = the workload's config)")
+    ap.add_argument("--hard", type=int, default=None, help="negclip: hard-negative captions per GPU (default B/2)")
+    ap.add_argument("--pacl-mode", choices=["ones", "sigmoid_rope_after"], default="ones")
+    ap.add_argument("--sparc-rope", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8, help="pairs per CPU-baseline run")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"error: WORLD_SIZE={world} but --gpus={args.gpus}")
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    t0 = time.time()
+    W = BUILDERS[args.workload](args, dev, rank, world)
+    engine, step = W["engine"], W["step"]
+    B = W["pairs"]
+    log(f"[rank {rank}] {args.workload}: setup {time.time() - t0:.1f}s, batch {B}/GPU, world {world}")
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -144,14 +311,14 @@ def main():
     if timing:
         # untimed profile pass: every kernel bracketed by HIP events -> per-kernel table (stderr) and
         # the dominant kernel; inside the timed region only that kernel's launches carry events
-        model.engine.set_timing(True)
+        engine.set_timing(True)
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-        profile = model.engine.kernel_stats()
-        model.engine.set_timing(False)
+        profile = engine.kernel_stats()
+        engine.set_timing(False)
         profile.sort(key=lambda s: -s["ms"])
-        model.engine.set_timing(True, only=profile[0]["name"])
+        engine.set_timing(True, only=profile[0]["name"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -162,9 +329,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    stats = model.engine.kernel_stats() if timing else []
+    stats = engine.kernel_stats() if timing else []
     if timing:
-        model.engine.set_timing(False)
+        engine.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -176,8 +343,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    pairs = world * B * args.steps
-    value = pairs / elapsed
+    value = world * B * args.steps / elapsed
     roof = None
     if stats:
         stats.sort(key=lambda s: -s["ms"])
@@ -185,15 +351,15 @@ def main():
         log("  per-kernel (profile pass, 2 steps, every launch bracketed by HIP events):")
         for s in profile:
             per = s["ms"] / max(1, s["launches"])
-            log(f"  {s['name']:<14} {s['ms'] / 2:9.3f} ms/step  {100 * s['ms'] / total_ms:5.1f}%  "
+            log(f"  {s['name']:<16} {s['ms'] / 2:9.3f} ms/step  {100 * s['ms'] / total_ms:5.1f}%  "
                 f"{s['launches'] // 2:4d} launches/step  "
                 f"{(s['flops'] / s['launches']) / (per * 1e-3) / 1e12 if s['flops'] else 0:8.1f} TFLOP/s  "
                 f"{(s['bytes'] / s['launches']) / (per * 1e-3) / 1e9:8.1f} GB/s")
         top = stats[0]
         per_ms = top["ms"] / top["launches"]
+        log(f"  timed region: {top['name']} {top['launches']} launches, avg {per_ms:.4f} ms")
         if top["flops"] > 0:
             ach = (top["flops"] / top["launches"]) / (per_ms * 1e-3) / 1e12
-            log(f"  timed region: {top['name']} {top['launches']} launches, avg {per_ms:.4f} ms")
             roof = {"bound": "mfma", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                     "traffic": load_traffic(top["name"]), "avg_launch_ms": round(per_ms, 4),
@@ -202,15 +368,25 @@ def main():
             ach = (top["bytes"] / top["launches"]) / (per_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": load_traffic(top["name"])}
-        roof["step_mfma_frac"] = round(value * FLOPS_PER_PAIR / 1e12 / world / PEAK_BF16_TFLOPS, 4)
+        roof["step_mfma_frac"] = round(value * W["flops_per_pair"] / 1e12 / world / PEAK_BF16_TFLOPS, 4)
+        hk = W.get("hbm_kernel")
+        if hk:
+            hs = [s for s in profile if s["name"] == hk]
+            if hs:
+                s = hs[0]
+                per = s["ms"] / s["launches"]
+                gbs = (s["bytes"] / s["launches"]) / (per * 1e-3) / 1e9
+                roof["hbm_kernel"] = {"kernel": hk, "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                      "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": round(per, 4),
+                                      "bytes_per_launch": s["bytes"] / s["launches"]}
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(sd, cfg, args.cpu_pairs)
+    if world == 1 and not args.no_cpu_baseline and args.workload == "clip":
+        cpu = cpu_baseline(W["sd"], W["cfg"], args.cpu_batch)
         cpu["vs_gpu"] = round(value / cpu["value"], 1)
 
     out = {
-        "metric": "image-text pairs/sec ViT-L/14-336",
+        "metric": W["metric"],
         "value": round(value, 2),
         "unit": "pairs/s",
         "n_gpus": world,
@@ -222,11 +398,7 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (deterministic uniform 336x336 images, 5-40 token captions; random-init weights)",
-        "config": {"workload": "CLIP ViT-L/14-336 encode_image + encode_text + normalise + contrastive logits "
-                               "(BASELINE configs[1]: batch 256/GPU bf16)",
-                   "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
-                   "parallelism": f"dp{world}",
-                   "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none"},
+        "config": W["config"],
         "roofline": roof,
         "cpu_baseline": cpu,
     }

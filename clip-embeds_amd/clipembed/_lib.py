@@ -90,6 +90,11 @@ _SIGNATURES = {
                                 POINTER(c_double), POINTER(c_double)]),
     "ce_kernel_gemm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                     c_void_p, c_int]),
+    "ce_kernel_gemm_bf16_epi": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                        c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ce_kernel_ln_stats_finalize": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
+    "ce_set_gemm_auto": (c_int, [c_int]),
+    "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),
     "ce_set_gemm_splitk": (c_int, [c_int]),
     "ce_set_ln_fold": (c_int, [c_void_p, c_int, POINTER(c_int)]),

@@ -5,6 +5,7 @@ Class names and forward signatures follow the reference so eval drivers read the
   open_clip_pacl_rope       pacl.py:184-197 (RoPE on the 1024-d patch tokens before the head)
   open_clip_pacl_rope_after pacl.py:199-209 (RoPE on projected tokens, sigmoid(10 cos) weights)
   sparc                     pacl.py:380-478 (forward / scoring / forward_text mask)
+  sparc_rope                pacl.py:480-484 (RoPE on the patch tokens before the visual head)
   apply_rope                pacl.py:147-181
   ClipLoss, SparcLoss       pacl.py:486-584 (temperature-scaled CLIP loss; SPARC global + masked local)
 Everything runs through libclipembed; the fused pooling is ce_pacl_pool.
@@ -170,16 +171,29 @@ class sparc(open_clip_pacl):
         return out, mask
 
     @torch.no_grad()
-    def forward(self, images, caps):
+    def align(self, v_patch_embed, l_token_embed):
+        """The similarity / min-max / threshold / alignment-weighting / grouping / L2 steps of
+        sparc.forward (pacl.py:455-476) on given patch [B,P,D] and token [B,T,D] embeddings (also the
+        train_sparc.py path with precomputed text embeddings).  Returns (grouped_normalised,
+        tokens_normalised)."""
         e = self.engine
-        v = self.forward_visual(images)
-        l, mask = self.forward_text(caps)
+        v = v_patch_embed.float().contiguous()
+        l = l_token_embed.float().contiguous()
         B, P, D = v.shape
         T = l.shape[1]
+        if l.shape[0] != B or l.shape[2] != D:
+            raise ValueError(f"sparc: patch {tuple(v.shape)} and token {tuple(l.shape)} embeddings do not match")
         grouped = torch.empty(B, T, D, device=e.device, dtype=torch.float32)
         l_norm = torch.empty_like(grouped)
         _lib.call("ce_sparc_forward", e.h, _stream(e.device), _ptr(v), _ptr(l), B, P, T, D, float(self.sigma),
                   _ptr(grouped), _ptr(l_norm), None)
+        return grouped, l_norm
+
+    @torch.no_grad()
+    def forward(self, images, caps):
+        v = self.forward_visual(images)
+        l, mask = self.forward_text(caps)
+        grouped, l_norm = self.align(v, l)
         return v, l_norm, grouped, mask
 
     @torch.no_grad()
@@ -194,6 +208,11 @@ class sparc(open_clip_pacl):
         else:
             gi = torch.nn.functional.normalize(g.mean(dim=1), dim=-1)
         return self.clip_model.logits(gi, gt, 1.0, with_text_logits=False)[0]
+
+
+class sparc_rope(sparc):
+    """sparc_rope (pacl.py:480-484): apply_rope on the 1024-d patch tokens before the visual head."""
+    rope = _lib.CE_ROPE_BEFORE
 
 
 class ClipLoss(torch.nn.Module):

@@ -84,7 +84,6 @@ def negclip_feature_grad(img: torch.Tensor, txt: torch.Tensor, scale: float, ran
         dist.all_gather(tparts, padded)
         # originals of every rank, then hard negatives of every rank (loss.py:144-153)
         all_txt = torch.cat([p[:B] for p in tparts] + [p[B:n] for p, n in zip(tparts, sizes)]).contiguous()
-        off_h = world * B + sum(n - B for n in sizes[:rank])
     else:
         all_img, all_txt = img, txt
     li = torch.arange(B, device=dev, dtype=torch.long) + (B * rank if world > 1 else 0)
@@ -93,10 +92,20 @@ def negclip_feature_grad(img: torch.Tensor, txt: torch.Tensor, scale: float, ran
     cgrad(img, all_txt, scale, li, 1.0 / B, None, d_all_txt, 0.5)    # CE(logits_per_image, li)
     cgrad(txt, all_img, scale, lt, 1.0 / B, dtxt, None, 0.5)         # CE(logits_per_text, lt)
     if world > 1:
-        dist.all_reduce(d_all_txt)                 # backward of the all-gather: sum over ranks
-        dtxt[:B] += d_all_txt[rank * B:(rank + 1) * B]
-        if T > B:
-            dtxt[B:] += d_all_txt[off_h:off_h + T - B]
+        # backward of the all-gather = reduce-scatter: lay the gradient out in the
+        # gather's padded per-rank chunks [originals of rank r | its hard negatives | zeros], sum
+        # over ranks and keep this rank's chunk — half the bytes of an all-reduce of the whole
+        mx = max(sizes)
+        dpad = torch.zeros(world, mx, txt.shape[1], device=dev, dtype=d_all_txt.dtype)
+        oh = world * B
+        for r, n in enumerate(sizes):
+            dpad[r, :B] = d_all_txt[r * B:(r + 1) * B]
+            if n > B:
+                dpad[r, B:n] = d_all_txt[oh:oh + n - B]
+            oh += n - B
+        mine = torch.empty(mx, txt.shape[1], device=dev, dtype=d_all_txt.dtype)
+        dist.reduce_scatter_tensor(mine, dpad.view(world * mx, -1))
+        dtxt += mine[:T]
     else:
         dtxt += d_all_txt
     return dtxt

@@ -1722,6 +1722,49 @@ int ce_kernel_gemm_bf16(void* stream, const void* A, const void* Wt, int M, int 
     return check_launch(ce::launch_gemm(p, act, out_dtype == CE_BF16, (hipStream_t)stream), "gemm");
 }
 
+int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* Wt, int M, int N, int K, const float* bias,
+                            int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
+                            void* stats_part, const void* fold_stats, const float* fold_c) {
+    if (epi == ce::EPI_PLAIN) return ce_kernel_gemm_bf16(stream, A, Wt, M, N, K, bias, act, resid, out, out_dtype);
+    if (!A || !Wt || !out) return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: null argument");
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 64)
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: need M,N,K > 0, K %% 64 == 0, N %% 64 == 0 (got %d %d %d)",
+                    M, N, K);
+    ce::GemmParams p{};
+    p.A = (const bf16_t*)A; p.lda = K; p.W = (const bf16_t*)Wt; p.ldw = K;
+    p.M = M; p.N = N; p.K = K; p.bias = bias; p.resid = resid; p.ldr = N; p.out = out; p.ldo = N;
+    p.part = ce::gemm_kernel_api_workspace(&p.part_elems);
+    if (epi == ce::EPI_LN_STATS) {
+        if (act != 0 || !resid || out_dtype != CE_F32 || !xb || !stats_part)
+            return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: LN stats needs act 0, resid, f32 out, xb, stats_part");
+        p.xb = (bf16_t*)xb;
+        p.stats_part = (float2*)stats_part;
+    } else if (epi == ce::EPI_LN_FOLD) {
+        if (act < 0 || act > 2 || resid || out_dtype != CE_BF16 || !bias || !fold_stats || !fold_c)
+            return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: LN fold needs no resid, bf16 out, bias, fold_stats, fold_c");
+        p.fold_stats = (const float2*)fold_stats;
+        p.fold_c = fold_c;
+    } else {
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: unknown epilogue %d", epi);
+    }
+    return check_launch(ce::launch_gemm(p, act, out_dtype == CE_BF16, (hipStream_t)stream, epi), "gemm_epi");
+}
+
+int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab) {
+    if (!stats || !part) return fail(CE_ERR_INVALID, "ce_kernel_ln_stats_finalize: null argument");
+    if (rows <= 0 || nslab <= 0 || nslab > 64) return fail(CE_ERR_INVALID, "ce_kernel_ln_stats_finalize: bad sizes");
+    return check_launch(ce::launch_ln_stats_finalize((float2*)stats, (const float2*)part, rows, nslab, (hipStream_t)stream),
+                        "ln_stats_finalize");
+}
+
+int ce_set_gemm_auto(int mode) { return ce::set_gemm_auto(mode); }
+int ce_gemm_path_counts(int64_t* counts, int n, int reset) {
+    if (n > 0 && !counts) return fail(CE_ERR_INVALID, "ce_gemm_path_counts: null counts");
+    long long tmp[ce::GEMM_PATH_COUNT];
+    ce::gemm_path_counts(tmp, ce::GEMM_PATH_COUNT, reset != 0);
+    for (int i = 0; i < n && i < ce::GEMM_PATH_COUNT; ++i) counts[i] = tmp[i];
+    return CE_OK;
+}
 int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
 int ce_set_gemm_splitk(int enable) { return ce::set_gemm_splitk(enable); }
 int ce_set_ln_fold(ce_handle* h, int enable, int* previous) {

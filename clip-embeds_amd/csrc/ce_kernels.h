@@ -43,6 +43,10 @@ hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t 
 hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s);
 int set_gemm_schedule(int v);   // returns previous
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
+int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 QKV-shape -> SCHED 11, ...); returns previous
+// launch counters per kernel path; index = path base + epilogue (EPI_PLAIN/LN_STATS/LN_FOLD)
+enum GemmPath { GEMM_PATH_W4PP = 0, GEMM_PATH_NT = 3, GEMM_PATH_FIXUP = 6, GEMM_PATH_OTHER = 9, GEMM_PATH_COUNT = 10 };
+void gemm_path_counts(long long* out, int n, bool reset);
 float* gemm_kernel_api_workspace(long* elems);   // per-device partial-tile buffer (kernel-level API)
 constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a handle provides (64 MB)
 

@@ -23,6 +23,7 @@
 #include "ce_kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #ifndef CE_RESID_RING
@@ -1417,12 +1418,17 @@ int w4pp_grid(int nwg) {
 // serially (c_fc + fold + GELU 35.9 vs 34.4, c_proj + stats 30.0 vs 29.3, out-proj 14.0 vs 12.8;
 // profiles/r01_gemm_w4p_sched10_11.log).  CE_GEMM_AUTO=0 pins SCHED 1, =2 sends every large
 // grid to SCHED 11.  Only for grids of >= 4 tiles per CU.
-bool auto_w4pp(const GemmParams& p, int act, bool resid) {
-    static int on = -1;
-    if (on < 0) {
+int g_auto = -1;
+int gemm_auto() {
+    if (g_auto < 0) {
         const char* e = getenv("CE_GEMM_AUTO");
-        on = e ? atoi(e) : 1;
+        g_auto = e ? atoi(e) : 1;
+        if (g_auto < 0 || g_auto > 3) g_auto = 1;
     }
+    return g_auto;
+}
+bool auto_w4pp(const GemmParams& p, int act, bool resid) {
+    const int on = gemm_auto();
     if (!on || gemm_sched() != 1) return false;
     // enough tiles that the persistent grid's last-round imbalance stays small (small grids keep
     // SCHED 1 and its split-K tail)
@@ -1433,6 +1439,12 @@ bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     return act == ACT_NONE && !resid;
 }
 
+// Launch counters per kernel path (ce_gemm_path_counts): lets the parity tests assert that the
+// instantiations a configuration selects by default (e.g. SCHED 11 + LN fold, split-K + LN stats at
+// B = 256) are the ones they just checked.
+std::atomic<long long> g_path[GEMM_PATH_COUNT];
+inline void count_path(int path) { g_path[path].fetch_add(1, std::memory_order_relaxed); }
+
 // LN-fold / LN-stats epilogues exist for SCHED 1 and SCHED 11
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
@@ -1441,6 +1453,7 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         p.gm = gemm_groupm();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
         hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+        count_path(GEMM_PATH_W4PP + EPI);
         return hipGetLastError();
     }
     p.gm = gemm_groupm();
@@ -1450,8 +1463,11 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     plan_tail(p, nwg);
     hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
                        dim3(nwg - p.tail + p.tail * p.split), dim3(NTHREADS), 0, s, p);
-    if (p.tail > 0)
+    count_path(GEMM_PATH_NT + EPI);
+    if (p.tail > 0) {
         hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
+        count_path(GEMM_PATH_FIXUP + EPI);
+    }
     return hipGetLastError();
 }
 
@@ -1472,9 +1488,12 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
             else
                 hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(grid), dim3(NTHREADS), 0, s, p);
             hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
+            count_path(GEMM_PATH_NT);
+            count_path(GEMM_PATH_FIXUP);
             return hipGetLastError();
         }
     }
+    count_path(sc == 11 ? GEMM_PATH_W4PP : sc == 1 ? GEMM_PATH_NT : GEMM_PATH_OTHER);
     if (sc == 9) {
         // one workgroup per CU (a multiple of 8 so every XCD group is complete)
         int grid = (num_cus() / 8) * 8;
@@ -1511,6 +1530,19 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
 }
 
 }  // namespace
+
+int set_gemm_auto(int mode) {
+    const int prev = gemm_auto();
+    g_auto = (mode >= 0 && mode <= 3) ? mode : 1;
+    return prev;
+}
+
+void gemm_path_counts(long long* out, int n, bool reset) {
+    for (int i = 0; i < GEMM_PATH_COUNT; ++i) {
+        const long long v = reset ? g_path[i].exchange(0) : g_path[i].load();
+        if (i < n) out[i] = v;
+    }
+}
 
 int set_gemm_splitk(int on) {
     const int prev = splitk_enabled() ? 1 : 0;

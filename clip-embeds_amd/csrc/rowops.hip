@@ -251,6 +251,12 @@ __global__ __launch_bounds__(256) void ce_rows_k(float* accum, const float* logi
     if (row >= R) return;
     const int64_t lab = labels[row];
     if (lab == -100) return;
+    if (lab < 0 || lab >= C) {
+        // F.cross_entropy raises on a label outside [0, C): poison the loss instead of reading
+        // past the row (no host sync on the label values)
+        if (lane == 0) atomicAdd(&accum[0], NAN);
+        return;
+    }
     const float* lr = logits + (size_t)row * C;
     float mx = -INFINITY;
     for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lr[c]);

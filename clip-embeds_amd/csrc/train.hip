@@ -463,9 +463,12 @@ __global__ __launch_bounds__(256) void ce_grad_k(float* __restrict__ g, const fl
     const float* zr = z + (size_t)r * C;
     float* gr = g + (size_t)r * C;
     const long lab = labels[r];
-    if (lab < 0) {
-        for (int j = lane; j < C; j += 64) gr[j] = 0.f;
-        if (lane == 0) { rowstat[r] = 0.f; rowstat[R + r] = 0.f; }
+    if (lab == -100 || lab < 0 || lab >= C) {
+        // -100 = ignore_index; any other label outside [0, C) (F.cross_entropy raises) poisons the
+        // row's gradient and loss with NaN rather than reading past the row
+        const float v = lab == -100 ? 0.f : NAN;
+        for (int j = lane; j < C; j += 64) gr[j] = v;
+        if (lane == 0) { rowstat[r] = v; rowstat[R + r] = v; }
         return;
     }
     float m = -INFINITY;

@@ -155,7 +155,8 @@ int ce_get_logits(ce_handle* h, void* stream, const float* img, int Bi, const fl
  * Replaces: F.cross_entropy(logits, labels) with ignore_index -100 as used by
  *   ClipLoss.forward (open_clip/src/open_clip/loss.py:172-193, labels :113-135) and the
  *   PACL ClipLoss (pacl.py:503-514).
- * logits f32 [R,C] device; labels int64 [R] device (-100 = ignored);
+ * logits f32 [R,C] device; labels int64 [R] device (-100 = ignored; any other label outside [0, C),
+ * where F.cross_entropy raises, makes the loss NaN: the device values are not read on the host);
  * out_loss: device f32 scalar = mean over non-ignored rows of (logsumexp - logit[label]). */
 int ce_cross_entropy(ce_handle* h, void* stream, const float* logits, int R, int C,
                      const int64_t* labels, float* out_loss);
@@ -248,6 +249,28 @@ int ce_set_gemm_schedule(int schedule);
 /* Split-K tail of the GEMM (default on): when a grid's last round holds few tiles, those tiles are
  * computed as K-chunks summed by a fixup launch.  Returns the previous setting.  For A/B. */
 int ce_set_gemm_splitk(int enable);
+/* Shape policy of the default GEMM schedule (env CE_GEMM_AUTO at first use): 0 = every GEMM on
+ * the 4-phase schedule (with its split-K tail), 1 = the default (grids of >= 4 tiles per CU with
+ * no activation and no residual, i.e. the vision QKV GEMM, on the four-wave persistent schedule),
+ * 2 = every large grid on it, 3 = large grids without a residual.  Returns the previous mode.
+ * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
+int ce_set_gemm_auto(int mode);
+/* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
+ * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
+ * schedules, and epi 0 = plain, 1 = LN statistics, 2 = LN fold.  n <= 10 entries are written. */
+int ce_gemm_path_counts(int64_t* counts, int n, int reset);
+/* GEMM with an LN-fold / LN-stats epilogue (the folded ResidualAttentionBlock,
+ * transformer.py:257-268), as the engine launches it:
+ *   epi 1 (LN stats): out f32 = A W^T + bias + resid; xb = bf16(out); stats_part[m][n/64] = (mean,
+ *         sum of squared deviations) of row m's 64-column slab n/64.  act must be 0.
+ *   epi 2 (LN fold):  out bf16 = act(fold_stats[m].y * (A W^T - fold_stats[m].x * fold_c[n]) + bias[n]).
+ * epi 0 is ce_kernel_gemm_bf16. */
+int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
+                            int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
+                            void* stats_part, const void* fold_stats, const float* fold_c);
+/* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
+ * stats [rows] float2, part [rows][nslab] float2. */
+int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab);
 /* LayerNorm folding of the image tower (default on; env CE_LN_FOLD=0 turns it off at ce_create):
  * ln_1/ln_2 of every visual block are folded into the in_proj/c_fc weights at ce_load_weights,
  * and the residual GEMMs emit the row statistics, so no LayerNorm launch remains inside the

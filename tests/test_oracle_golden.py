@@ -130,3 +130,23 @@ def test_negclip_two_ranks(golden):
         np.testing.assert_allclose(got, g[f"hard_r{r}"], rtol=1e-5)
         plain = O.negclip_local_loss(imgs, [t[:B] for t in txts], B, r, 14.2857)
         np.testing.assert_allclose(plain, g[f"plain_local_r{r}"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("tag,name,layers", [("clip_v2t2", "ViT-L-14-336", (2, 2)),
+                                             ("clip_quickgelu_v1t1", "ViT-L-14-336-quickgelu", (1, 1))])
+def test_torch_cpu_baseline_vs_golden(golden, tag, name, layers):
+    """The torch f32 CPU restatement bench.py times as the reference's CPU path
+    (oracle/clip_torch_cpu.py: the reference's own ATen calls) is pinned to the same goldens."""
+    from oracle.clip_torch_cpu import TorchCLIP
+    cfg = get_model_config(name).with_depth(*layers)
+    g = golden(tag)
+    sd = W.synthetic_state_dict(cfg)
+    m = TorchCLIP(sd, cfg)
+    pi = m.encode_image(W.synthetic_images(2, seed=1000)).numpy()
+    pt = m.encode_text(g["captions"]).numpy()
+    assert rel(pi, g["image_pooled"]) < 2e-5
+    assert rel(pt, g["text_pooled"]) < 2e-5
+    fi = m.encode_image(W.synthetic_images(2, seed=1000), normalize=True)
+    ft = m.encode_text(g["captions"], normalize=True)
+    il, _ = m.get_logits(fi, ft, float(g["logit_scale_exp"]))
+    np.testing.assert_allclose(il.numpy(), g["image_logits"], rtol=1e-5, atol=1e-4)
