@@ -83,6 +83,8 @@ _SIGNATURES = {
                               c_int, c_float, c_float, c_float, c_void_p]),
     "ce_preprocess_images": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                      c_int, c_void_p]),
+    "ce_preprocess_images_boxes": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_int, c_int, c_void_p]),
     "ce_apply_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "ce_set_kernel_timing": (c_int, [c_void_p, c_int]),
     "ce_set_kernel_timing_filter": (c_int, [c_void_p, c_char_p]),
@@ -94,6 +96,7 @@ _SIGNATURES = {
                                         c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ce_kernel_ln_stats_finalize": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     "ce_set_gemm_auto": (c_int, [c_int]),
+    "ce_set_gemm_trace": (c_int, [c_void_p, c_int64]),
     "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),
     "ce_set_gemm_splitk": (c_int, [c_int]),

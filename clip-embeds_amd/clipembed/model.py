@@ -313,13 +313,17 @@ def create_model(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = N
 
 def create_model_and_transforms(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = None,
                                 device=None, **kw):
-    """Returns (model, preprocess_train, preprocess_val) like open_clip (factory.py:822-958).
-    preprocess_val is the device eval transform (clipembed.transforms.image_transform: Pillow-exact
-    bicubic resize, center crop, normalise); preprocess_train (RandomResizedCrop augmentation) is
-    not on the device path and is None."""
+    """Returns (model, preprocess_train, preprocess_val) like open_clip (factory.py:822-958), both
+    transforms on the device (clipembed.transforms.image_transform): preprocess_val = Pillow-exact
+    bicubic resize + center crop + normalise; preprocess_train = RandomResizedCrop(scale=(0.9, 1.0))
+    with the box drawn from the host torch RNG and the bicubic resample on the device.  eval_clip.py
+    takes the SECOND value (eval_clip.py:21-24), so its What'sUp / MMVP scores use the train one."""
     from .transforms import image_transform
+    aug_cfg = kw.pop("aug_cfg", None)
     model = create_model(model_name, pretrained, device, **kw)
-    return model, None, image_transform(model.cfg.vision.image_size, is_train=False, device=device)
+    S = model.cfg.vision.image_size
+    return (model, image_transform(S, is_train=True, aug_cfg=aug_cfg, device=device),
+            image_transform(S, is_train=False, device=device))
 
 
 def load_checkpoint_file(path: str) -> dict:

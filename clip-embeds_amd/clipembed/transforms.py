@@ -3,6 +3,9 @@
   image_transform(336, is_train=False)   open_clip/src/open_clip/transform.py:274-389 (eval path,
                                          resize_mode 'shortest', bicubic): Resize -> CenterCrop ->
                                          ToTensor -> Normalize(OpenAI)
+  image_transform(336, is_train=True)    transform.py:334-355: RandomResizedCrop(scale=(0.9, 1.0),
+                                         BICUBIC) -> ToTensor -> Normalize(OpenAI); box from the
+                                         host torch RNG, resample on the device
   prepare_data(...).preprocess_image     Patch-Aligned-Contrastive-Learning/data/utils.py:30-52:
                                          ToTensor -> Resize((S,S)) -> Normalize(ImageNet)
 
@@ -13,6 +16,7 @@ launch).  JPEG/PNG decoding stays on the host.
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Sequence
 
 import numpy as np
@@ -54,6 +58,9 @@ class DeviceImageProcessor:
 
     @torch.no_grad()
     def batch(self, imgs: Sequence[np.ndarray]) -> torch.Tensor:
+        return self._run(imgs, None)
+
+    def _run(self, imgs: Sequence[np.ndarray], boxes: Optional[np.ndarray]) -> torch.Tensor:
         dev = self.device if self.device is not None else torch.device("cuda", torch.cuda.current_device())
         e = self.engine if self.engine is not None else kernel_engine(dev)
         sizes = [x.nbytes for x in imgs]
@@ -69,10 +76,65 @@ class DeviceImageProcessor:
         S = self.image_size
         out = torch.empty(len(imgs), 3, S, S, device=e.device, dtype=self.out_dtype)
         dt = _lib.CE_BF16 if self.out_dtype == torch.bfloat16 else _lib.CE_F32
-        _lib.call("ce_preprocess_images", e.h, _stream(e.device), _ptr(dev), offsets.ctypes.data,
-                  heights.ctypes.data, widths.ctypes.data, len(imgs), self.mode, dt, _ptr(out))
+        if boxes is None:
+            _lib.call("ce_preprocess_images", e.h, _stream(e.device), _ptr(dev), offsets.ctypes.data,
+                      heights.ctypes.data, widths.ctypes.data, len(imgs), self.mode, dt, _ptr(out))
+        else:
+            boxes = np.ascontiguousarray(boxes, np.int32)
+            _lib.call("ce_preprocess_images_boxes", e.h, _stream(e.device), _ptr(dev), offsets.ctypes.data,
+                      heights.ctypes.data, widths.ctypes.data, boxes.ctypes.data, len(imgs), dt, _ptr(out))
         dev.record_stream(torch.cuda.current_stream(e.device))
         return out
+
+
+def random_resized_crop_params(height: int, width: int, scale=(0.9, 1.0), ratio=(3.0 / 4.0, 4.0 / 3.0),
+                               generator: Optional[torch.Generator] = None):
+    """torchvision RandomResizedCrop.get_params (third-party, the transform open_clip's training
+    preprocess builds, transform.py:334-340; torchvision is not imported here): the same torch RNG
+    draws in the same order — per attempt two uniform_ draws, then two randint draws on success —
+    so a seeded run picks the reference's boxes.  Returns (top, left, height, width)."""
+    area = height * width
+    log_ratio = torch.log(torch.tensor(ratio))
+    for _ in range(10):
+        target_area = area * torch.empty(1).uniform_(scale[0], scale[1], generator=generator).item()
+        aspect_ratio = torch.exp(torch.empty(1).uniform_(log_ratio[0], log_ratio[1], generator=generator)).item()
+        w = int(round(math.sqrt(target_area * aspect_ratio)))
+        h = int(round(math.sqrt(target_area / aspect_ratio)))
+        if 0 < w <= width and 0 < h <= height:
+            i = torch.randint(0, height - h + 1, size=(1,), generator=generator).item()
+            j = torch.randint(0, width - w + 1, size=(1,), generator=generator).item()
+            return i, j, h, w
+    in_ratio = float(width) / float(height)           # fallback: central crop
+    if in_ratio < min(ratio):
+        w = width
+        h = int(round(w / min(ratio)))
+    elif in_ratio > max(ratio):
+        h = height
+        w = int(round(h * max(ratio)))
+    else:
+        w, h = width, height
+    return (height - h) // 2, (width - w) // 2, h, w
+
+
+class DeviceTrainProcessor(DeviceImageProcessor):
+    """open_clip's training preprocess (transform.py:334-355 with the default AugmentationCfg:
+    RandomResizedCrop(S, scale=(0.9, 1.0), BICUBIC) -> RGB -> ToTensor -> Normalize(OpenAI)): the crop
+    box is drawn on the host from the torch RNG (random_resized_crop_params, one image at a time in
+    list order, as the reference's per-image calls do), the bicubic resample of the box runs on the
+    device (ce_preprocess_images_boxes, Pillow-exact).  eval_clip.py:21-24 feeds this object to
+    prepare_data_clip, so it is what the What'sUp / MMVP drivers preprocess with."""
+
+    def __init__(self, image_size: int = 336, scale=(0.9, 1.0), ratio=(3.0 / 4.0, 4.0 / 3.0), device=None,
+                 out_dtype=torch.float32, engine=None, generator: Optional[torch.Generator] = None):
+        super().__init__(_lib.CE_PRE_CLIP_BICUBIC, image_size, device, out_dtype, engine)
+        self.scale, self.ratio, self.generator = tuple(scale), tuple(ratio), generator
+
+    @torch.no_grad()
+    def batch(self, imgs: Sequence[np.ndarray]) -> torch.Tensor:
+        boxes = np.array([random_resized_crop_params(x.shape[0], x.shape[1], self.scale, self.ratio, self.generator)
+                          for x in imgs], np.int32).reshape(-1, 4)
+        self.last_boxes = boxes          # (top, left, height, width) per image of the last call
+        return self._run(imgs, boxes)
 
 
 def image_transform(image_size=336, is_train: bool = False, mean: Optional[Sequence[float]] = None,
@@ -80,15 +142,27 @@ def image_transform(image_size=336, is_train: bool = False, mean: Optional[Seque
                     interpolation: Optional[str] = None, fill_color: int = 0, aug_cfg=None, device=None,
                     engine=None):
     """open_clip image_transform (transform.py:274-389), eval path on the device."""
+    from .weights import OPENAI_MEAN, OPENAI_STD
     if isinstance(image_size, (tuple, list)):
         if image_size[0] != image_size[1]:
             raise NotImplementedError("non-square image_size (ResizeKeepRatio) is not on the device path")
         image_size = image_size[0]
     if is_train:
-        raise NotImplementedError("training augmentations (RandomResizedCrop, jitter) are not on the device path")
+        # open_clip's default AugmentationCfg (transform.py:62-72,334-355); jitter / grayscale / timm
+        # augmentations are not on the device path
+        scale, ratio = (0.9, 1.0), (3.0 / 4.0, 4.0 / 3.0)
+        if aug_cfg is not None:
+            cfg = aug_cfg if isinstance(aug_cfg, dict) else vars(aug_cfg)
+            extra = {k for k, v in cfg.items() if v and k not in ("scale", "ratio")}
+            if extra:
+                raise NotImplementedError(f"training augmentations {sorted(extra)} are not on the device path")
+            scale = tuple(cfg.get("scale") or scale)
+            ratio = tuple(cfg.get("ratio") or ratio)
+        if (mean is not None and tuple(mean) != tuple(OPENAI_MEAN)) or (std is not None and tuple(std) != tuple(OPENAI_STD)):
+            raise NotImplementedError("the device path normalises with the OpenAI mean/std (constants.py:1-2)")
+        return DeviceTrainProcessor(image_size, scale, ratio, device, engine=engine)
     if (resize_mode or "shortest") != "shortest" or (interpolation or "bicubic") != "bicubic":
         raise NotImplementedError("only resize_mode='shortest' with bicubic interpolation is on the device path")
-    from .weights import OPENAI_MEAN, OPENAI_STD
     if (mean is not None and tuple(mean) != tuple(OPENAI_MEAN)) or (std is not None and tuple(std) != tuple(OPENAI_STD)):
         raise NotImplementedError("the device path normalises with the OpenAI mean/std (constants.py:1-2)")
     return DeviceImageProcessor(_lib.CE_PRE_CLIP_BICUBIC, image_size, device, engine=engine)

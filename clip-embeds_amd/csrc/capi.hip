@@ -1564,13 +1564,18 @@ int grow_pinned(char*& buf, size_t& bytes, size_t need) {
 
 }  // namespace
 
-int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
-                         const int* heights, const int* widths, int B, int mode, int out_dtype, void* out) {
+namespace {
+
+// boxes: null, or per image (top, left, height, width) of a crop resized to S x S (CLIP bicubic only)
+int preprocess_impl(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets, const int* heights,
+                    const int* widths, const int* boxes, int B, int mode, int out_dtype, void* out) {
     if (!h || !images || !offsets || !heights || !widths || !out)
         return fail(CE_ERR_INVALID, "ce_preprocess_images: null argument");
     if (B <= 0) return fail(CE_ERR_INVALID, "ce_preprocess_images: batch must be positive (got %d)", B);
     if (mode != CE_PRE_CLIP_BICUBIC && mode != CE_PRE_PACL_BILINEAR_AA)
         return fail(CE_ERR_INVALID, "ce_preprocess_images: unknown mode %d", mode);
+    if (boxes && mode != CE_PRE_CLIP_BICUBIC)
+        return fail(CE_ERR_INVALID, "ce_preprocess_images: crop boxes need the CLIP bicubic mode");
     if (out_dtype != CE_F32 && out_dtype != CE_BF16)
         return fail(CE_ERR_INVALID, "ce_preprocess_images: output must be f32 or bf16");
     const int S = h->cfg.image_size;
@@ -1589,7 +1594,26 @@ int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, cons
         m.H = H;
         m.W = Wd;
         m.bx_off = (int)bounds.size();
-        if (!pacl) {
+        if (boxes) {
+            // torchvision F.resized_crop on a PIL image: img.crop((left, top, left + w, top + h))
+            // .resize((S, S), BICUBIC) -> Pillow's resampler over the crop, both axes to S
+            const int top = boxes[4 * b], left = boxes[4 * b + 1], bh = boxes[4 * b + 2], bw = boxes[4 * b + 3];
+            if (top < 0 || left < 0 || bh <= 0 || bw <= 0 || top + bh > H || left + bw > Wd)
+                return fail(CE_ERR_INVALID, "ce_preprocess_images: crop box %d (%d,%d,%d,%d) outside the %dx%d image", b,
+                            top, left, bh, bw, H, Wd);
+            m.kx_off = (int)itaps.size();
+            m.ksx = pil_taps(bw, S, 0, S, -left, bounds, itaps);
+            std::vector<int> vb, vt;
+            const int ksy = pil_taps(bh, S, 0, S, -top, vb, vt);
+            m.ybase = vb[0];
+            m.nrows = vb[2 * (S - 1)] + vb[2 * (S - 1) + 1] - m.ybase;
+            for (int i = 0; i < S; ++i) vb[2 * i] -= m.ybase;
+            m.by_off = (int)bounds.size();
+            bounds.insert(bounds.end(), vb.begin(), vb.end());
+            m.ky_off = (int)itaps.size();
+            m.ksy = ksy;
+            itaps.insert(itaps.end(), vt.begin(), vt.end());
+        } else if (!pacl) {
             // torchvision Resize(S) shortest edge (_compute_resized_output_size) + CenterCrop(S)
             // offsets int(round(d / 2.0)) with round-half-even
             const bool wshort = Wd <= H;
@@ -1658,6 +1682,20 @@ int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, cons
                                                   pacl ? kImagenetMean : kOpenaiMean, pacl ? kImagenetStd : kOpenaiStd,
                                                   out, s);
                  });
+}
+
+}  // namespace
+
+int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
+                         const int* heights, const int* widths, int B, int mode, int out_dtype, void* out) {
+    return preprocess_impl(h, stream, images, offsets, heights, widths, nullptr, B, mode, out_dtype, out);
+}
+
+int ce_preprocess_images_boxes(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
+                               const int* heights, const int* widths, const int* boxes, int B, int out_dtype,
+                               void* out) {
+    if (!boxes) return fail(CE_ERR_INVALID, "ce_preprocess_images_boxes: null boxes");
+    return preprocess_impl(h, stream, images, offsets, heights, widths, boxes, B, CE_PRE_CLIP_BICUBIC, out_dtype, out);
 }
 
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out) {
@@ -1758,6 +1796,11 @@ int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int
 }
 
 int ce_set_gemm_auto(int mode) { return ce::set_gemm_auto(mode); }
+int ce_set_gemm_trace(void* buf, int64_t n_blocks) {
+    if (n_blocks < 0) return fail(CE_ERR_INVALID, "ce_set_gemm_trace: negative size");
+    ce::set_gemm_trace((unsigned long long*)buf, (long)n_blocks);
+    return CE_OK;
+}
 int ce_gemm_path_counts(int64_t* counts, int n, int reset) {
     if (n > 0 && !counts) return fail(CE_ERR_INVALID, "ce_gemm_path_counts: null counts");
     long long tmp[ce::GEMM_PATH_COUNT];

@@ -35,6 +35,13 @@ struct GemmParams {
     float2* stats_part = nullptr;
     const float2* fold_stats = nullptr;
     const float* fold_c = nullptr;
+    // de-synchronisation of the first round of workgroups (set by launch_gemm): blocks b in
+    // [stagger_lo, stagger_hi) with bit `stagger_bit` of b set (stagger_bit < 0: all of them) sleep
+    // `stagger` x 127 x 64 cycles before starting, so that later rounds keep half the CUs in their
+    // epilogue while the other half run MFMAs instead of the whole chip alternating between the two
+    int stagger = 0, stagger_lo = 0, stagger_hi = 0, stagger_bit = -1;
+    unsigned long long* trace = nullptr;   // diagnostic timeline, [block][4] (set_gemm_trace)
+    int trace_n = 0;
 };
 enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
@@ -45,8 +52,10 @@ int set_gemm_schedule(int v);   // returns previous
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
 int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 QKV-shape -> SCHED 11, ...); returns previous
 // launch counters per kernel path; index = path base + epilogue (EPI_PLAIN/LN_STATS/LN_FOLD)
-enum GemmPath { GEMM_PATH_W4PP = 0, GEMM_PATH_NT = 3, GEMM_PATH_FIXUP = 6, GEMM_PATH_OTHER = 9, GEMM_PATH_COUNT = 10 };
+enum GemmPath { GEMM_PATH_W4PP = 0, GEMM_PATH_NT = 3, GEMM_PATH_FIXUP = 6, GEMM_PATH_OTHER = 9, GEMM_PATH_W2 = 10,
+                GEMM_PATH_COUNT = 13 };
 void gemm_path_counts(long long* out, int n, bool reset);
+void set_gemm_trace(unsigned long long* buf, long n);   // diagnostics: per-block timeline of the next launches
 float* gemm_kernel_api_workspace(long* elems);   // per-device partial-tile buffer (kernel-level API)
 constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a handle provides (64 MB)
 

@@ -299,6 +299,29 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (
 }
 
 
+// Diagnostic timeline (ce_set_gemm_trace): wave 0 of each workgroup records s_memrealtime (100 MHz,
+// chip-wide) at start, after the K-loop and after its epilogue, plus the hardware id word, into
+// its own buffer (nothing else reads it).  Null in normal runs.
+__device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot_idx) {
+    if (p.trace && threadIdx.x == 0 && blockIdx.x < p.trace_n) {
+        unsigned long long* r = p.trace + (size_t)blockIdx.x * 4;
+        r[slot_idx] = __builtin_amdgcn_s_memrealtime();
+        if (slot_idx == 0) {
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            r[3] = ((unsigned long long)xcc << 32) | hw;
+        }
+    }
+}
+
+__device__ __forceinline__ void stagger_sleep(const GemmParams& p) {
+    const int b = blockIdx.x;
+    if (p.stagger > 0 && b >= p.stagger_lo && b < p.stagger_hi && (p.stagger_bit < 0 || ((b >> p.stagger_bit) & 1)))
+        for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
 // Bijective XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous range
 // of tile ids so the tiles that share A / W panels run on one L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -611,6 +634,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_persist(GemmParams p) {
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED, int RING = CE_RESID_RING, int EPI = EPI_PLAIN>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    trace_stamp(p, 0);
+    stagger_sleep(p);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -835,8 +860,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
                 *reinterpret_cast<f32x4*>(dst + (size_t)i * 16 * BN + j * 16) = acc[i][j];
         return;
     }
+    trace_stamp(p, 1);
     gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, RING, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane,
                                                            PRE ? &fold : nullptr);
+    trace_stamp(p, 2);
 }
 
 // Split-K tail fixup: sums the `split` partial slabs of each tail tile in fixed order (deterministic)
@@ -1320,14 +1347,179 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------------------------------
+// SCHED 12 ("w2"): TWO 256-thread workgroups per CU, each computing a 256 x 128 tile with four
+// waves of 128 x 64 (2 x 2; acc[8][4] of v_mfma_f32_16x16x32_bf16, the SCHED 1 per-wave tile and
+// epilogue layout).  72 KB of LDS per workgroup (a 3-slot ring of BK = 32 stages: A 256 x 64 B,
+// W 128 x 64 B), so two workgroups fit a CU and one's epilogue (GELU / LN fold / residual /
+// LN stats) runs beside the other's MFMAs — SCHED 1 and 11 run one workgroup per CU and leave the
+// matrix pipe idle for the whole epilogue.  Per K-step: counted vmcnt (the step after this one
+// stays in flight), one barrier, the DMA of step t+2 into the slot step t-1 used, 12 fragment
+// reads, 32 MFMAs.  LDS image: 64-B rows, 16-B chunk c of row r at c ^ (2 * ((r >> 3) & 1)) —
+// conflict-free for the four 16-lane groups of ds_read_b128 (tools/lds_bank_sim.py); the DMA
+// source address carries the inverse permutation.
+constexpr int W2_BN = 128, W2_BK = 32;
+constexpr int W2_A_BYTES = BM * W2_BK * 2;          // 16 KB
+constexpr int W2_SLOT = (BM + W2_BN) * W2_BK * 2;   // 24 KB
+constexpr int W2_NSLOT = 3;
+#ifndef CE_W2_SOLO
+#define CE_W2_SOLO 0     // diagnostic build: pad LDS so one workgroup runs per CU
+#endif
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_w2(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[CE_W2_SOLO ? 2 * W2_NSLOT * W2_SLOT : W2_NSLOT * W2_SLOT];
+    trace_stamp(p, 0);
+    stagger_sleep(p);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = (p.N + W2_BN - 1) / W2_BN;
+    const int nwg = tiles_m * tiles_n;
+    const int wgid = xcd_remap(blockIdx.x, nwg);
+    int tm, tn;
+    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
+    const int m0 = tm * BM, n0 = tn * W2_BN;
+    const int nk = p.K / W2_BK;
+
+    // staging: instruction j (0..5) of wave w moves 16 rows x 64 B; j < 4: A rows 16(4j+w) + (lane>>2),
+    // else W rows 16(4(j-4)+w) + (lane>>2); LDS chunk lane&3 holds source chunk (lane&3) ^ f(row)
+    const int srow = lane >> 2;
+    const int schunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
+    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
+    const __amdgpu_buffer_rsrc_t srdW =
+        make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, W2_BN)) * (int)p.ldw * 2);
+    int voff[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int g = j < 4 ? 4 * j + wave : 4 * (j - 4) + wave;
+        const int row = 16 * g + srow;
+        voff[j] = row * (int)(j < 4 ? p.lda : p.ldw) * 2 + schunk * 16;
+    }
+    auto dma = [&](int kt) {
+        char* base = smem + (kt % W2_NSLOT) * W2_SLOT;
+        const int kb = kt * W2_BK * 2;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int g = j < 4 ? 4 * j + wave : 4 * (j - 4) + wave;
+            if (j < 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + g * 1024), 16, voff[j], kb, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + W2_A_BYTES + g * 1024), 16,
+                                                         voff[j], kb, 0, 0);
+        }
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int fo = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
+    const int a_off = wm * 128 * 64 + fo;
+    const int w_off = W2_A_BYTES + wn * 64 * 64 + fo;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Two phases per K-step t, one barrier each:
+    //   A: MFMA rows 0-3 (alo, b[t])   | reads ahi (rows 4-7) of t, DMA of step t+2
+    //      lgkmcnt(0), vmcnt(step t+1 landed), barrier
+    //   B: MFMA rows 4-7 (ahi, b[t])   | reads alo and b of step t+1
+    // The DMA of step t+2 goes into the slot of step t-1, whose last reads (ahi in phase A of t-1)
+    // retired before that phase's barrier.  b is double-buffered (bx / by by the parity of t).
+    bf16x8 alo[4], ahi[4], bx[4], by[4];
+    auto rd = [&](bf16x8 (&d)[4], const char* sb, int off, int i0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = *reinterpret_cast<const bf16x8*>(sb + off + (i0 + q) * 16 * 64);
+    };
+    auto slot = [&](int kt) { return smem + (kt % W2_NSLOT) * W2_SLOT; };
+    auto mf = [&](int i0, const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i0 + i][j], 0, 0, 0);
+    };
+    auto step = [&](int kt, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
+        const char* sb = slot(kt);
+        // ---- phase A ----
+        mf(0, alo, bc);
+        rd(ahi, sb, a_off, 4);
+        const bool pf = kt + 2 < nk;
+        if (pf) dma(kt + 2);
+#pragma unroll
+        for (int g2 = 0; g2 < 4; ++g2) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int g2 = 0; g2 < 6; ++g2) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (pf) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- phase B ----
+        mf(4, ahi, bc);
+        if (kt + 1 < nk) {
+            const char* sn = slot(kt + 1);
+            rd(bn, sn, w_off, 0);
+            rd(alo, sn, a_off, 0);
+        }
+#pragma unroll
+        for (int g2 = 0; g2 < 8; ++g2) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    dma(0);
+    if (nk > 1) {
+        dma(1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    rd(bx, smem, w_off, 0);
+    rd(alo, smem, a_off, 0);
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+        step(kt, bx, by);
+        step(kt + 1, by, bx);
+    }
+    if (kt < nk) step(kt, bx, by);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    trace_stamp(p, 1);
+    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>(
+        p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+    trace_stamp(p, 2);
+}
+
 int g_sched = -1;
 int g_ring = CE_RESID_RING;     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
+unsigned long long* g_trace = nullptr;
+long g_trace_n = 0;
+int g_stagger = -1;             // first-round de-synchronisation sleep (units of s_sleep 127)
+int gemm_stagger() {
+    if (g_stagger < 0) {
+        const char* e = getenv("CE_GEMM_STAGGER");
+        g_stagger = e ? std::max(0, atoi(e)) : 0;
+    }
+    return g_stagger;
+}
 int gemm_sched() {
     if (g_sched < 0) {
         const char* e = getenv("CE_GEMM_SCHED");
         g_sched = e ? atoi(e) : 1;
         if (!(g_sched == 0 || g_sched == 1 || g_sched == 2 || g_sched == 3 || g_sched == 4 || g_sched == 6 ||
-              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11))
+              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11 || g_sched == 12))
             g_sched = 1;
     }
     return g_sched;
@@ -1446,9 +1638,38 @@ std::atomic<long long> g_path[GEMM_PATH_COUNT];
 inline void count_path(int path) { g_path[path].fetch_add(1, std::memory_order_relaxed); }
 
 // LN-fold / LN-stats epilogues exist for SCHED 1 and SCHED 11
+// SCHED 1 (one workgroup per CU): half the CUs of every XCD (bit 3 of the block id: blocks b and
+// b + 8 share an XCD) start their first tile late
+void set_stagger_1(GemmParams& p, int nwg) {
+    if (nwg <= 2 * num_cus()) return;
+    p.stagger = gemm_stagger();
+    p.stagger_lo = 0;
+    p.stagger_hi = num_cus();
+    p.stagger_bit = 3;
+}
+
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
+hipError_t launch_w2(const GemmParams& p0, hipStream_t s) {
+    GemmParams p = p0;
+    p.gm = gemm_groupm();
+    p.tail = 0;
+    p.split = 1;
+    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + W2_BN - 1) / W2_BN);
+    if (nwg > 2 * num_cus()) {     // the second workgroup of each CU starts half a tile late
+        p.stagger = gemm_stagger();
+        p.stagger_lo = num_cus();
+        p.stagger_hi = 2 * num_cus();
+        p.stagger_bit = -1;
+    }
+    hipLaunchKernelGGL((gemm_bf16_w2<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(nwg), dim3(256), 0, s, p);
+    count_path(GEMM_PATH_W2 + EPI);
+    return hipGetLastError();
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
+    if (gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     if (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID)) {
         p.gm = gemm_groupm();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -1461,6 +1682,7 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     p.tail = 0;
     p.split = 1;
     plan_tail(p, nwg);
+    set_stagger_1(p, nwg);
     hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
                        dim3(nwg - p.tail + p.tail * p.split), dim3(NTHREADS), 0, s, p);
     count_path(GEMM_PATH_NT + EPI);
@@ -1477,8 +1699,10 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : gemm_sched();
+    if (sc == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
     p.tail = 0;
     p.split = 1;
+    if (sc == 1) set_stagger_1(p, nwg);
     if (sc == 1) {
         plan_tail(p, nwg);
         if (p.tail > 0) {
@@ -1557,14 +1781,24 @@ float* gemm_kernel_api_workspace(long* elems) {
 
 int set_gemm_schedule(int v) {
     const int prev = gemm_sched() | (gemm_groupm() << 8);
-    const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff;
+    const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff, st = (v >> 24) & 0x7f;
     if (ring >= 2 && ring <= 5) g_ring = ring;
-    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 || sc == 11) ? sc : 1;
+    if (st) g_stagger = st - 1;
+    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 || sc == 11 ||
+               sc == 12) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }
 
-hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi) {
+void set_gemm_trace(unsigned long long* buf, long n) {
+    g_trace = buf;
+    g_trace_n = buf ? n : 0;
+}
+
+hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t s, int epi) {
+    GemmParams p = p0;
+    p.trace = g_trace;
+    p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;

@@ -210,6 +210,14 @@ int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l,
 enum ce_preprocess_mode { CE_PRE_CLIP_BICUBIC = 0, CE_PRE_PACL_BILINEAR_AA = 1 };
 int ce_preprocess_images(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
                          const int* heights, const int* widths, int B, int mode, int out_dtype, void* out);
+/* The training transform's resample step (open_clip transform.py:334-355: RandomResizedCrop(S,
+ * scale=(0.9, 1.0), BICUBIC) -> ToTensor -> Normalize(OpenAI)); the caller draws the crop boxes on
+ * the host (torchvision RandomResizedCrop.get_params with the torch RNG) and the device applies
+ * torchvision's F.resized_crop on a PIL image: Pillow's bicubic resampler (bit-exact) from the box
+ * (top, left, height, width) of image b to S x S.  boxes: HOST int32 [B][4], inside each image. */
+int ce_preprocess_images_boxes(ce_handle* h, void* stream, const uint8_t* images, const int64_t* offsets,
+                               const int* heights, const int* widths, const int* boxes, int B, int out_dtype,
+                               void* out);
 
 /* SparcLoss.forward (Patch-Aligned-Contrastive-Learning/model/pacl.py:564-584, masked local loss
  * :527-562): global_weight (reference 0.5, :520) * CLIP loss (logit scale 1/temperature) of the
@@ -243,7 +251,8 @@ int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* t
 int ce_kernel_gemm_bf16(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                         int act, const float* resid, void* out, int out_dtype);
 /* Select the GEMM main-loop schedule for subsequent launches (bits 0-7: 0 = 2-stage whole-tile
- * ring, 1 = 4-phase half-tile ring, the default; bits 8-15: tile-order M-group, 0 = keep);
+ * ring, 1 = 4-phase half-tile ring, the default; bits 8-15: tile-order M-group, 0 = keep; bits 24-30:
+ * 1 + first-round stagger in units of s_sleep 127 (~8k cycles) for half the CUs, 0 = keep);
  * returns the previous value in the same encoding.  For A/B measurement. */
 int ce_set_gemm_schedule(int schedule);
 /* Split-K tail of the GEMM (default on): when a grid's last round holds few tiles, those tiles are
@@ -257,7 +266,8 @@ int ce_set_gemm_splitk(int enable);
 int ce_set_gemm_auto(int mode);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
- * schedules, and epi 0 = plain, 1 = LN statistics, 2 = LN fold.  n <= 10 entries are written. */
+ * schedules, 10 = two-workgroup 256 x 128 (SCHED 12), and epi 0 = plain, 1 = LN statistics, 2 = LN
+ * fold.  n <= 13 entries are written. */
 int ce_gemm_path_counts(int64_t* counts, int n, int reset);
 /* GEMM with an LN-fold / LN-stats epilogue (the folded ResidualAttentionBlock,
  * transformer.py:257-268), as the engine launches it:
@@ -268,6 +278,10 @@ int ce_gemm_path_counts(int64_t* counts, int n, int reset);
 int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                             int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
                             void* stats_part, const void* fold_stats, const float* fold_c);
+/* Diagnostics: when buf (device, n_blocks x 4 uint64) is non-null, the SCHED 1 / SCHED 12 GEMM
+ * kernels record per workgroup {s_memrealtime at start, after the K-loop, after wave 0's epilogue,
+ * (XCC id << 32) | HW_ID} for blocks < n_blocks.  Null turns it off. */
+int ce_set_gemm_trace(void* buf, int64_t n_blocks);
 /* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
  * stats [rows] float2, part [rows][nslab] float2. */
 int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab);

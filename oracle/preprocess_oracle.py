@@ -122,6 +122,16 @@ def clip_eval_preprocess(img: np.ndarray, size: int = 336) -> np.ndarray:
     return to_tensor_normalize(r[top:top + size, left:left + size], OPENAI_MEAN, OPENAI_STD)
 
 
+def clip_train_preprocess(img: np.ndarray, box, size: int = 336) -> np.ndarray:
+    """open_clip's training preprocess (transform.py:334-355) for a given RandomResizedCrop box
+    (top, left, height, width): torchvision F.resized_crop on a PIL image = Image.crop then
+    Image.resize((size, size), BICUBIC), then ToTensor -> Normalize(OpenAI)."""
+    top, left, h, w = (int(v) for v in box)
+    crop = np.ascontiguousarray(img[top:top + h, left:left + w])
+    r = crop if (h, w) == (size, size) else pil_resize_bicubic(crop, size, size)
+    return to_tensor_normalize(r, OPENAI_MEAN, OPENAI_STD)
+
+
 # ------------------------------------------------------------------ torch antialiased bilinear
 def aa_bilinear_weights(in_size: int, out_size: int):
     """ATen _compute_weights_aa (bilinear, align_corners=False) in float32: (xmin, xsize, w)."""

@@ -29,7 +29,7 @@ ROWS_V = [0, 1, 23, 24, 287, 300, 551, 575]
 COS_TOL = 1e-3
 PATH_TOL = 2e-4
 # ce_gemm_path_counts indices (include/clipembed.h)
-W4PP, NT, FIXUP = 0, 3, 6
+W4PP, NT, FIXUP, W2 = 0, 3, 6, 10
 PLAIN, STATS, FOLD = 0, 1, 2
 
 
@@ -42,8 +42,8 @@ def S():
 
 
 def path_counts(reset=True):
-    c = (ctypes.c_int64 * 10)()
-    _lib.call("ce_gemm_path_counts", c, 10, 1 if reset else 0)
+    c = (ctypes.c_int64 * 13)()
+    _lib.call("ce_gemm_path_counts", c, 13, 1 if reset else 0)
     return list(c)
 
 
@@ -62,7 +62,7 @@ def _operands(M, N, K, seed):
     return g, A, Wt, bias
 
 
-@pytest.mark.parametrize("N,act,expect", [(3072, 0, W4PP + FOLD), (4096, 1, NT + FOLD)])
+@pytest.mark.parametrize("N,act,expect", [(3072, 0, W4PP + FOLD), (4096, 1, NT + FOLD), (4096, 1, W2 + FOLD)])
 def test_ln_fold_epilogue_at_bench_shape(N, act, expect):
     """QKV (N = 3072, no activation -> SCHED 11) and c_fc (N = 4096, GELU -> SCHED 1) with the
     LN-fold epilogue: out = act(rstd_m (A W^T - mu_m c_n) + d_n), vs torch f32."""
@@ -74,9 +74,13 @@ def test_ln_fold_epilogue_at_bench_shape(N, act, expect):
     fold_c = Wt.float().sum(1).contiguous()
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     path_counts()
-    _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(Wt), M, N, K, P(bias), act, None, P(out), _lib.CE_BF16,
-              FOLD, None, None, P(stats), P(fold_c))
-    torch.cuda.synchronize()
+    prev = _lib.lib().ce_set_gemm_schedule(12 if expect == W2 + FOLD else 1)
+    try:
+        _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(Wt), M, N, K, P(bias), act, None, P(out), _lib.CE_BF16,
+                  FOLD, None, None, P(stats), P(fold_c))
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().ce_set_gemm_schedule(prev)
     cnt = path_counts()
     assert cnt[expect] == 1 and sum(cnt) == 1, cnt
     ref = rstd[:, None] * (A.float() @ Wt.float().t() - mu[:, None] * fold_c[None, :]) + bias

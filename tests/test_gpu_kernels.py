@@ -36,7 +36,7 @@ def gemm_ref(A, W, bias, act, resid):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 1024), (4617, 3072, 1024), (1154, 1024, 4096),
                                    (231, 2304, 768), (5, 768, 1024), (700, 832, 640), (1, 64, 64)])
 @pytest.mark.parametrize("variant", ["bias_bf16", "gelu_bf16", "qgelu_bf16", "resid_f32", "plain_f32"])
-@pytest.mark.parametrize("sched", [1, 2, 0, 6, 9, 10, 11])
+@pytest.mark.parametrize("sched", [1, 2, 0, 6, 9, 10, 11, 12])
 def test_gemm(M, N, K, variant, sched):
     prev = _lib.lib().ce_set_gemm_schedule(sched)
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)

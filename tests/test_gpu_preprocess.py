@@ -85,3 +85,31 @@ def test_errors():
     with pytest.raises(ClipEmbedError, match="unknown mode"):
         _lib.call("ce_preprocess_images", e.h, _stream(e.device), _ptr(buf), off.ctypes.data, one.ctypes.data,
                   one.ctypes.data, 1, 7, _lib.CE_F32, _ptr(out))
+
+
+def test_clip_train_crop_bit_exact(images):
+    """create_model_and_transforms(...)[1] (eval_clip.py:21-24 feeds it to prepare_data_clip): the
+    RandomResizedCrop box from the host torch RNG, the bicubic resample on the device — bit-exact
+    against the Pillow-pinned oracle for the same boxes (same seed)."""
+    import clipembed
+    from clipembed.transforms import DeviceTrainProcessor, random_resized_crop_params
+    _, train, val = clipembed.create_model_and_transforms("ViT-L-14-336")
+    assert isinstance(train, DeviceTrainProcessor) and not isinstance(val, DeviceTrainProcessor)
+    torch.manual_seed(77)
+    out = train(images).cpu().numpy()                 # one launch, boxes drawn per image in order
+    torch.manual_seed(77)
+    for i, img in enumerate(images):
+        box = random_resized_crop_params(img.shape[0], img.shape[1])
+        ref = P.clip_train_preprocess(img, box)
+        assert np.array_equal(out[i], ref), f"image {i} box {box}: max |d| {np.abs(out[i] - ref).max()}"
+    from clipembed import ClipEmbedError, _lib
+    from clipembed.model import kernel_engine, _ptr, _stream
+    e = kernel_engine("cuda")
+    buf = torch.zeros(48, dtype=torch.uint8, device="cuda")
+    o = torch.empty(1, 3, 336, 336, device="cuda")
+    off = np.zeros(1, np.int64)
+    hw = np.array([4], np.int32)
+    bad = np.array([[0, 2, 4, 3]], np.int32)        # left + width > 4
+    with pytest.raises(ClipEmbedError, match="outside"):
+        _lib.call("ce_preprocess_images_boxes", e.h, _stream(e.device), _ptr(buf), off.ctypes.data, hw.ctypes.data,
+                  hw.ctypes.data, bad.ctypes.data, 1, _lib.CE_F32, _ptr(o))

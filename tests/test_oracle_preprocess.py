@@ -48,3 +48,44 @@ def test_against_pillow_directly():
         for ow, oh in [(336, 336), (97, 401), (1000, 50)]:
             ref = np.asarray(Image.fromarray(img).resize((ow, oh), Image.BICUBIC))
             assert np.array_equal(P.pil_resize_bicubic(img, ow, oh), ref)
+
+
+def test_train_crop_against_pillow_directly():
+    """clip_train_preprocess = Pillow crop + BICUBIC resize to 336 (torchvision F.resized_crop on a PIL
+    image) + ToTensor/Normalize, for boxes drawn by clipembed's RandomResizedCrop parameter sampler."""
+    Image = pytest.importorskip("PIL.Image")
+    import torch
+    from clipembed.transforms import random_resized_crop_params
+    g = torch.Generator().manual_seed(3)
+    for i, (h, w) in enumerate([(480, 640), (336, 336), (200, 150)]):
+        img = mgp.image(i, h, w)
+        box = random_resized_crop_params(h, w, generator=g)
+        top, left, bh, bw = box
+        assert 0 <= top and top + bh <= h and 0 <= left and left + bw <= w
+        assert 0.9 * h * w * 0.95 <= bh * bw <= h * w          # scale (0.9, 1.0) up to rounding
+        ref = np.asarray(Image.fromarray(img).crop((left, top, left + bw, top + bh)).resize((336, 336), Image.BICUBIC))
+        x = ref.transpose(2, 0, 1).astype(np.float32) / np.float32(255)
+        m = np.asarray(P.OPENAI_MEAN, np.float32)[:, None, None]
+        s = np.asarray(P.OPENAI_STD, np.float32)[:, None, None]
+        assert np.array_equal(P.clip_train_preprocess(img, box), ((x - m) / s).astype(np.float32))
+
+
+def test_random_resized_crop_params_rng_stream():
+    """Same torch RNG draws as torchvision's RandomResizedCrop.get_params: two uniform_ draws per
+    attempt then two randint draws; the fallback (10 rejected attempts) is a central crop."""
+    import math
+    import torch
+    from clipembed.transforms import random_resized_crop_params
+    torch.manual_seed(11)
+    box = random_resized_crop_params(480, 640)
+    torch.manual_seed(11)
+    ta = 480 * 640 * torch.empty(1).uniform_(0.9, 1.0).item()
+    lr = torch.log(torch.tensor((3 / 4, 4 / 3)))
+    ar = torch.exp(torch.empty(1).uniform_(lr[0], lr[1])).item()
+    w, h = int(round(math.sqrt(ta * ar))), int(round(math.sqrt(ta / ar)))
+    if 0 < w <= 640 and 0 < h <= 480:
+        i = torch.randint(0, 480 - h + 1, size=(1,)).item()
+        j = torch.randint(0, 640 - w + 1, size=(1,)).item()
+        assert box == (i, j, h, w)
+    # a 1 x 2000 strip can never host a crop of area >= 0.9 with ratio <= 4/3: central fallback
+    assert random_resized_crop_params(1, 2000) == (0, 999, 1, 1)        # h = 1, w = round(1 * 4/3)
