@@ -1,6 +1,6 @@
 // Small f32 contractions and the fused PACL / SPARC reductions for gfx950.
 //
-//  * fgemm: batched f32 GEMM (64x64 tiles, LDS-staged, 4x4 outputs per thread).  Used where the
+//  * fgemm: batched f32 GEMM on the f32-input matrix cores (64x64 tiles, 32x32x2 f32 MFMA).  Used where the
 //    reference keeps f32 and the work is tiny next to the towers: pooled @ proj
 //    (transformer.py:830-831, model.py:293-296), contrastive logits scale * I @ T^T
 //    (model.py:303-310, loss.py:155-164), PACL text Linear (pacl.py:75-79), SPARC's two einsums
@@ -19,6 +19,12 @@ namespace {
 constexpr int FT = 64;    // tile
 constexpr int FK = 16;    // k chunk
 
+// 64 x 64 output tile per 256-thread block; wave w computes the 32 x 32 quadrant (w >> 1, w & 1)
+// with v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate: bit-for-bit a k-ordered fmaf chain, i.e.
+// the reference's f32 precision at the matrix-core rate; guide §3 'FP32-input MFMA').  LDS holds
+// the K-chunk k-major (As[k][m], Bs[k][n]) so lane l reads A[m = l & 31][k = l >> 5] and
+// B[k = l >> 5][n = l & 31] for the instruction with consecutive lanes on consecutive words.
+// C/D: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) for register r.
 template <bool B_NK>
 __global__ __launch_bounds__(256) void fgemm_k(FGemmParams p) {
     __shared__ float As[FK][FT + 4];
@@ -28,56 +34,47 @@ __global__ __launch_bounds__(256) void fgemm_k(FGemmParams p) {
     const float* Bm = p.B + (size_t)z * p.sB;
     float* C = p.C + (size_t)z * p.sC;
     const int i0 = blockIdx.y * FT, j0 = blockIdx.x * FT;
-    const int tid = threadIdx.x;
-    const int ty = tid >> 4, tx = tid & 15;
-    float acc[4][4] = {};
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     for (int k0 = 0; k0 < p.K; k0 += FK) {
-        // A tile: 64 rows x 16 k  (each thread 4 elements)
         for (int e = tid; e < FT * FK; e += 256) {
             const int rr = e / FK, kk = e % FK;
             const int gi = i0 + rr, gk = k0 + kk;
             As[kk][rr] = (gi < p.M && gk < p.K) ? A[(size_t)gi * p.lda + gk] : 0.f;
         }
         for (int e = tid; e < FT * FK; e += 256) {
-            float v;
             if constexpr (B_NK) {
                 const int cc = e / FK, kk = e % FK;
                 const int gj = j0 + cc, gk = k0 + kk;
-                v = (gj < p.N && gk < p.K) ? Bm[(size_t)gj * p.ldb + gk] : 0.f;
-                Bs[kk][cc] = v;
+                Bs[kk][cc] = (gj < p.N && gk < p.K) ? Bm[(size_t)gj * p.ldb + gk] : 0.f;
             } else {
                 const int kk = e / FT, cc = e % FT;
                 const int gj = j0 + cc, gk = k0 + kk;
-                v = (gj < p.N && gk < p.K) ? Bm[(size_t)gk * p.ldb + gj] : 0.f;
-                Bs[kk][cc] = v;
+                Bs[kk][cc] = (gj < p.N && gk < p.K) ? Bm[(size_t)gk * p.ldb + gj] : 0.f;
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int kk = 0; kk < FK; ++kk) {
-            float a[4], b[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) { a[u] = As[kk][ty * 4 + u]; b[u] = Bs[kk][tx * 4 + u]; }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int w = 0; w < 4; ++w) acc[u][w] = fmaf(a[u], b[w], acc[u][w]);
+        for (int kk = 0; kk < FK; kk += 2) {
+            const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+            const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
         }
         __syncthreads();
     }
+    const int gj = j0 + wn * 32 + (lane & 31);
+    if (gj >= p.N) return;
+    const float bj = p.bias ? p.bias[gj] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int gi = i0 + ty * 4 + u;
+    for (int r = 0; r < 16; ++r) {
+        const int gi = i0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (gi >= p.M) continue;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const int gj = j0 + tx * 4 + w;
-            if (gj >= p.N) continue;
-            float v = acc[u][w] * p.alpha;
-            if (p.bias) v += p.bias[gj];
-            C[(size_t)gi * p.ldc + gj] = v;
-            if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
-        }
+        const float v = acc[r] * p.alpha + bj;
+        C[(size_t)gi * p.ldc + gj] = v;
+        if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
     }
 }
 

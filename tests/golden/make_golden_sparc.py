@@ -1,0 +1,81 @@
+"""Golden outputs of the reference SPARC model at real dimensions (D = 768, T = 77, P = 576) —
+build container only.
+
+Runs Patch-Aligned-Contrastive-Learning/model/pacl.py's `sparc` and `sparc_rope` (pacl.py:380-484)
+around the reference open_clip CLIP ViT-L/14-336 with 1-block towers (the SPARC math after the
+towers is depth-independent) and the deterministic synthetic weights / PACL-shaped heads, built
+without the network fetch in the constructor (the same head modules, pacl.py:397-406).  Writes
+outputs only: selected token / patch rows of forward(), both scoring() modes and SparcLoss.
+
+    python tests/golden/make_golden_sparc.py   ->  tests/golden/sparc_full.npz
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [HERE, os.path.join(REPO, "clip-embeds_amd"), REPO]
+
+import make_golden as MG  # noqa: E402
+
+ROWS_T = [0, 1, 5, 9, 20, 40, 76]
+ROWS_P = [0, 1, 23, 24, 287, 300, 550, 575]
+
+
+def build_sparc(pacl_mod, clip_model, cls, heads_sd, sigma):
+    import torch
+    from torch import nn
+    obj = cls.__new__(cls)
+    nn.Module.__init__(obj)
+    obj.sigma = sigma
+    obj.clip_model = clip_model
+    obj.visual_projection = nn.Sequential(nn.LayerNorm(1024), nn.Dropout(0.1), pacl_mod.Patch_Projection(1024, 768))
+    obj.text_projection = nn.Sequential(nn.LayerNorm(768), nn.Dropout(0.1), nn.Linear(768, 768))
+    for p in obj.clip_model.parameters():
+        p.requires_grad = False
+    obj.clip_model.visual.output_tokens = True
+    obj.clip_model.output_text_tokens = True
+    missing = obj.load_state_dict({k: torch.from_numpy(v) for k, v in heads_sd.items()}, strict=False)
+    assert not missing.unexpected_keys, missing.unexpected_keys
+    obj.eval()
+    return obj
+
+
+def main():
+    import torch
+    from clipembed import weights as W
+    from clipembed.config import get_model_config
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    model_mod, _, pacl_mod = MG.import_reference()
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    clip, _ = MG.build_clip(model_mod, cfg)
+    heads = W.synthetic_pacl_heads(cfg.with_pacl(768))
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1300))
+    caps = W.synthetic_captions(2, seed=2300)
+    caps[1] = W.synthetic_captions(1, seed=2301, min_len=7, max_len=7)[0]      # EOT at 8: short caption
+    caps = torch.from_numpy(caps)
+    out = {"captions": caps.numpy(), "images_sha": np.array(MG.sha(imgs.numpy()))}
+    with torch.no_grad():
+        for tag, cls in (("sparc", pacl_mod.sparc), ("sparc_rope", pacl_mod.sparc_rope)):
+            mod = build_sparc(pacl_mod, clip, cls, heads, 1.0 / 576)
+            v, l, g, mask = mod.forward(imgs, caps)
+            out[f"{tag}_v_rows"] = np.ascontiguousarray(v.numpy()[:, ROWS_P])
+            out[f"{tag}_v_sum"] = v.numpy().sum((1, 2))
+            out[f"{tag}_l_rows"] = np.ascontiguousarray(l.numpy()[:, ROWS_T])
+            out[f"{tag}_g_rows"] = np.ascontiguousarray(g.numpy()[:, ROWS_T])
+            out[f"{tag}_g_sum"] = g.numpy().sum((1, 2))
+            out[f"{tag}_mask"] = mask.numpy()
+            out[f"{tag}_score_local"] = mod.scoring(imgs, caps, local=True).numpy()
+            out[f"{tag}_score_global"] = mod.scoring(imgs, caps, local=False).numpy()
+            out[f"{tag}_score_bcast"] = mod.scoring(imgs[:1], caps, local=True).numpy()   # 1 image x 2 captions
+            out[f"{tag}_loss"] = np.float32(pacl_mod.SparcLoss(0.07)(v, l, g, mask).item())
+    path = os.path.join(HERE, "sparc_full.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

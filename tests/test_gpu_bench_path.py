@@ -209,3 +209,32 @@ def test_batch256_full_depth_bench_path(full_model, golden):
         assert np.isfinite(ti_n).all()
     finally:
         m.visual.output_tokens = False
+
+
+@pytest.mark.parametrize("tag", ["pacl", "pacl_rope_after"])
+def test_pacl_batch512_golden_rows(golden, tag):
+    """PACL forward at the C3 batch (512 pairs, BASELINE configs[2]) with the two golden pairs of
+    tests/golden/pacl.npz at rows 0 and 511 (2-block towers as in the fixture): those rows within
+    1e-3 cosine of the reference's open_clip_pacl outputs; every row finite and unit-norm."""
+    from clipembed.pacl import open_clip_pacl, open_clip_pacl_rope_after
+    cls = {"pacl": open_clip_pacl, "pacl_rope_after": open_clip_pacl_rope_after}[tag]
+    cfg = get_model_config("ViT-L-14-336").with_depth(2, 2)
+    g = golden("pacl")
+    mod = cls(cfg=cfg, clip_state_dict=W.synthetic_state_dict(cfg))
+    mod.load_state_dict(W.synthetic_pacl_heads(cfg.with_pacl(768)))
+    mod.to(DEV)
+    imgs = W.synthetic_images(512, seed=1200)
+    gi = W.synthetic_images(2, seed=1100)
+    imgs[0], imgs[511] = gi[0], gi[1]
+    caps = W.synthetic_captions(512, seed=2200)
+    caps[0], caps[511] = g["captions"][0], g["captions"][1]
+    path_counts()
+    a, b = mod(torch.from_numpy(imgs).to(DEV), torch.from_numpy(caps).to(DEV))
+    torch.cuda.synchronize()
+    cnt = path_counts()
+    assert cnt[W4PP + FOLD] == 2 and cnt[FIXUP + STATS] >= 1, cnt       # the big-grid paths ran
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    assert cos_dist(a[[0, 511]], g[f"{tag}_img"]) < COS_TOL
+    assert cos_dist(b[[0, 511]], g[f"{tag}_txt"]) < COS_TOL
+    assert np.isfinite(a).all() and np.isfinite(b).all()
+    np.testing.assert_allclose(np.linalg.norm(a, axis=-1), 1.0, rtol=1e-4)
