@@ -303,7 +303,7 @@ def create_model(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = N
     cfg = get_model_config(model_name)
     model = CLIP(cfg, output_dict=output_dict)
     if pretrained:
-        model.load_state_dict(load_checkpoint_file(pretrained))
+        load_checkpoint(model, pretrained)
     if state_dict is not None:
         model.load_state_dict(state_dict)
     if device is not None:
@@ -326,12 +326,83 @@ def create_model_and_transforms(model_name: str = "ViT-L-14-336", pretrained: Op
             image_transform(S, is_train=False, device=device))
 
 
-def load_checkpoint_file(path: str) -> dict:
-    if path.endswith(".safetensors"):
+def load_state_dict(checkpoint_path: str, device="cpu", weights_only: bool = True) -> dict:
+    """open_clip factory.load_state_dict (factory.py:143-168): .safetensors via safetensors, else
+    torch.load (weights_only by default); a {'state_dict': ...} wrapper is unwrapped, a TorchScript
+    module gives its state_dict minus input_resolution / context_length / vocab_size, and the
+    'module.' prefix is stripped from every key when the FIRST key starts with 'module'."""
+    if str(checkpoint_path).endswith(".safetensors"):
         from safetensors.torch import load_file
-        sd = load_file(path)
+        checkpoint = load_file(checkpoint_path, device=device)
     else:
-        sd = torch.load(path, map_location="cpu", weights_only=True)
-        if isinstance(sd, dict) and "state_dict" in sd:
-            sd = sd["state_dict"]
-    return {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
+        checkpoint = torch.load(checkpoint_path, map_location=device, weights_only=weights_only)
+    if isinstance(checkpoint, dict) and "state_dict" in checkpoint:
+        state_dict = checkpoint["state_dict"]
+    elif isinstance(checkpoint, torch.jit.ScriptModule):
+        state_dict = checkpoint.state_dict()
+        for key in ("input_resolution", "context_length", "vocab_size"):
+            state_dict.pop(key, None)
+    else:
+        state_dict = checkpoint
+    if next(iter(state_dict.items()))[0].startswith("module"):
+        state_dict = {k[7:]: v for k, v in state_dict.items()}
+    return state_dict
+
+
+def resize_pos_embed(state_dict: dict, model: "CLIP", interpolation: str = "bicubic", antialias: bool = True):
+    """open_clip resize_pos_embed (model.py:748-779): a checkpoint whose visual positional grid
+    differs from the model's is resampled with the same torch op (bicubic, antialias, on the host,
+    once at load time; 1 class token kept)."""
+    import torch.nn.functional as F
+    old = state_dict.get("visual.positional_embedding", None)
+    if old is None:
+        return
+    old = torch.as_tensor(old)
+    gh, gw = model.visual.grid_size
+    if gh * gw + 1 == old.shape[0]:
+        return
+    tok, img = old[:1], old[1:]
+    og = int(math.sqrt(len(img)))
+    img = img.reshape(1, og, og, -1).permute(0, 3, 1, 2)
+    img = F.interpolate(img.float(), size=(gh, gw), mode=interpolation, antialias=antialias, align_corners=False)
+    img = img.permute(0, 2, 3, 1).reshape(1, gh * gw, -1)[0].to(old.dtype)
+    state_dict["visual.positional_embedding"] = torch.cat([tok, img], dim=0)
+
+
+def resize_text_pos_embed(state_dict: dict, model: "CLIP", interpolation: str = "linear", antialias: bool = False):
+    """open_clip resize_text_pos_embed (model.py:782-812): text positional rows resampled to the
+    model's context length."""
+    import torch.nn.functional as F
+    old = state_dict.get("positional_embedding", None)
+    if old is None:
+        return
+    old = torch.as_tensor(old)
+    num_pos, width = model.cfg.text.context_length, model.cfg.text.width
+    if old.shape[1] != width:
+        raise ValueError("text pos_embed width changed!")
+    if old.shape[0] == num_pos:
+        return
+    x = old.reshape(1, old.shape[0], width).permute(0, 2, 1)
+    x = F.interpolate(x.float(), size=num_pos, mode=interpolation, antialias=antialias, align_corners=False)
+    state_dict["positional_embedding"] = x.permute(0, 2, 1)[0].to(old.dtype)
+
+
+def load_checkpoint(model: "CLIP", checkpoint_path: str, strict: bool = True, weights_only: bool = True,
+                    device="cpu"):
+    """open_clip factory.load_checkpoint (factory.py:171-215) for the registered CLIP configs:
+    load_state_dict, logit_scale reshaped to the model's (0-d) parameter, position embeddings
+    resized, then model.load_state_dict.  (3rd-party converters and big_vision .npz weights are
+    not on the path.)"""
+    state_dict = load_state_dict(checkpoint_path, device=device, weights_only=weights_only)
+    if "logit_scale" in state_dict and torch.as_tensor(state_dict["logit_scale"]).ndim != model.logit_scale.ndim:
+        state_dict["logit_scale"] = torch.as_tensor(state_dict["logit_scale"]).reshape(model.logit_scale.shape)
+    state_dict.pop("text.transformer.embeddings.position_ids", None)
+    resize_pos_embed(state_dict, model)
+    resize_text_pos_embed(state_dict, model)
+    model.load_state_dict(state_dict, strict=strict)
+    return model
+
+
+def load_checkpoint_file(path: str) -> dict:
+    """State dict of a local open_clip checkpoint (load_state_dict above)."""
+    return load_state_dict(path)
