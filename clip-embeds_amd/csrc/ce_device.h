@@ -20,8 +20,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
     return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
+// two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32, round-to-nearest-even, NaN stays NaN)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -84,6 +87,38 @@ __device__ __forceinline__ f32x2 gelu_pair(f32x2 x) {
     p = __builtin_elementwise_fma(p, t, (f32x2)(0.14136378f));
     const f32x2 phi = __builtin_elementwise_fma(u, p, (f32x2)(0.5f));
     return x * phi;
+}
+
+// GELU as x * sigmoid(z(x)) with z(x) = u * P(u^2), u = clamp(x, +-5), P a degree-4 fit of
+// logit(Phi) (times -log2 e, so the exponential is one v_exp_f32):  y = x / (1 + 2^(u * P(u^2))).
+// Error <= 9.5e-6 * max(1, |y|) vs the exact-erf GELU over all x in f32 (tests/test_host.py),
+// far below the bf16 rounding of the GEMM output it feeds.  9 VALU + 2 transcendental ops
+// (~52 issue cycles per value for one wave on a SIMD) vs 17 for the degree-12 polynomial above.
+// four independent values per call, so the dependent polynomial chains interleave
+__device__ __forceinline__ f32x4 gelu_fast4(f32x4 x) {
+    f32x4 u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) u[e] = __builtin_amdgcn_fmed3f(x[e], -5.0f, 5.0f);
+    const f32x4 u2 = u * u;
+    f32x4 p = __builtin_elementwise_fma(u2, (f32x4)(-4.781674761034083e-06f), (f32x4)(0.00011614440882112831f));
+    p = __builtin_elementwise_fma(p, u2, (f32x4)(0.00021269964054226875f));
+    p = __builtin_elementwise_fma(p, u2, (f32x4)(-0.10495619475841522f));
+    p = __builtin_elementwise_fma(p, u2, (f32x4)(-2.3021795749664307f));
+    const f32x4 z = u * p;
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = x[e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z[e]));
+    return y;
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float u = __builtin_amdgcn_fmed3f(x, -5.0f, 5.0f);
+    const float u2 = u * u;
+    float p = fmaf(u2, -4.781674761034083e-06f, 0.00011614440882112831f);
+    p = fmaf(p, u2, 0.00021269964054226875f);
+    p = fmaf(p, u2, -0.10495619475841522f);
+    p = fmaf(p, u2, -2.3021795749664307f);
+    const float e = __builtin_amdgcn_exp2f(u * p);
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2 };

@@ -42,6 +42,7 @@ struct GemmParams {
     int stagger = 0, stagger_lo = 0, stagger_hi = 0, stagger_bit = -1;
     unsigned long long* trace = nullptr;   // diagnostic timeline, [block][4] (set_gemm_trace)
     int trace_n = 0;
+    int variant = 0;                       // kernel-variant bits for A/B (set_gemm_variant)
 };
 enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
@@ -50,6 +51,7 @@ hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t 
 hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s);
 int set_gemm_schedule(int v);   // returns previous
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
+int set_gemm_variant(int bits);  // kernel-variant bits for A/B (GEMM_VAR_*); returns previous
 int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 QKV-shape -> SCHED 11, ...); returns previous
 // launch counters per kernel path; index = path base + epilogue (EPI_PLAIN/LN_STATS/LN_FOLD)
 enum GemmPath { GEMM_PATH_W4PP = 0, GEMM_PATH_NT = 3, GEMM_PATH_FIXUP = 6, GEMM_PATH_OTHER = 9, GEMM_PATH_W2 = 10,

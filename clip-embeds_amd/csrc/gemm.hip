@@ -23,6 +23,7 @@
 #include "ce_kernels.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 #include <cstdlib>
 
@@ -108,6 +109,12 @@ struct FoldOps {
 
 #ifndef CE_FOLD_PREFETCH
 #define CE_FOLD_PREFETCH 0
+#endif
+
+// kernel-variant bits (set_gemm_variant / env CE_GEMM_VARIANT), default GEMM_VAR_DEFAULT
+enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2 };
+#ifndef CE_GEMM_VAR_DEFAULT
+#define CE_GEMM_VAR_DEFAULT GEMM_VAR_W4PP_NOWAIT
 #endif
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
@@ -299,12 +306,118 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (
 }
 
 
+// ------------------------------------------------------------------------------------------
+// Four-wave (SCHED 11) epilogue for bf16 outputs without a residual (QKV / c_fc: bias or LN fold,
+// optional activation).  Lane holds acc[i][j] = C[mbase + 16i + fr][nbase + 16j + 4fq .. +3].
+// Written for one wave per SIMD, where nothing hides a stall:
+//  * every load it needs (bias, fold columns, row statistics) is issued before its first store —
+//    vmcnt retires loads and stores in issue order, so a load issued after stores would wait for
+//    all of them;
+//  * stores go through a buffer descriptor based at the quadrant's first row whose size ends at row
+//    M: rows past M are dropped by the hardware range check, so there is no per-row branch, and the
+//    addresses are one 32-bit VGPR (row-pair step added to it, 16-column step in the immediate);
+//  * two fragment rows are paired with v_permlane16_swap so each lane stores 16 B (8 columns).
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+template <int ACT>
+__device__ __forceinline__ float w4_act(float v) {
+    if constexpr (ACT == ACT_GELU) return gelu_fast(v);
+    else return apply_act<ACT>(v);
+}
+
+// Per-wave side area of the four-wave kernel's LDS (after the two 64-KB stage buffers): bias and
+// LN-fold column sums of the wave's 128 columns, (mu, rstd) of its 128 rows.  Filled by LDS-DMA
+// during the tile's last K-tile (retired by that K-tile's own vmcnt wait), read by ds_read in the
+// epilogue, so the epilogue issues no global load at all.
+constexpr int W4_SIDE_BYTES = 3 * 1024;     // [bias 512 B + pad][fold_c 512 B + pad][stats 1 KB]
+
+template <int EPI>
+__device__ __forceinline__ void w4_side_fill(const GemmParams& p, char* side, int mbase, int nbase, int lane) {
+    const __amdgpu_buffer_rsrc_t bsrd = make_srd(p.bias ? (const void*)p.bias : (const void*)p.A, p.bias ? p.N * 4 : 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(bsrd, (CE_LDS void*)side, 16, (nbase + lane * 4) * 4, 0, 0, 0);
+    if constexpr (EPI == EPI_LN_FOLD) {
+        const __amdgpu_buffer_rsrc_t csrd = make_srd(p.fold_c, p.N * 4);
+        const __amdgpu_buffer_rsrc_t ssrd = make_srd(p.fold_stats, p.M * 8);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(csrd, (CE_LDS void*)(side + 1024), 16, (nbase + lane * 4) * 4, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ssrd, (CE_LDS void*)(side + 2048), 16, (mbase + lane * 2) * 8, 0, 0, 0);
+    }
+}
+
+template <int ACT, int EPI, int JN>
+__device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase, int nbase,
+                                                   int lane, const char* side) {
+    const int fr = lane & 15, fq = lane >> 4;
+    const int rows = max(0, min(p.M - mbase, 128));
+    const __amdgpu_buffer_rsrc_t osrd =
+        make_srd(static_cast<bf16_t*>(p.out) + (size_t)mbase * p.ldo, rows * (int)p.ldo * 2);
+    const int ldo2 = (int)p.ldo * 2;
+    int voff = (fr + (fq & 1) * 16) * ldo2 + (fq >> 1) * 16 + nbase * 2;
+    // column operands of all JN 16-column blocks up front (one LDS latency, not one per block)
+    const float4* sb = reinterpret_cast<const float4*>(side) + fq;            // bias[16j + 4fq ..]
+    const float4* sc = reinterpret_cast<const float4*>(side + 1024) + fq;     // fold_c
+    const float2* ss = reinterpret_cast<const float2*>(side + 2048) + fr;     // (mu, rstd) of row 16i + fr
+    float4 bv[JN], cv[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        bv[j] = sb[4 * j];
+        if constexpr (EPI == EPI_LN_FOLD) cv[j] = sc[4 * j];
+    }
+    float2 st[8];
+    if constexpr (EPI == EPI_LN_FOLD) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = ss[16 * i];
+    }
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) {
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+            uint2 h[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                f32x4 v = acc[2 * ip + r][j];
+                const float4 b = bv[j];
+                if constexpr (EPI == EPI_LN_FOLD) {
+                    const float4 c = cv[j];
+                    const float2 t = st[2 * ip + r];
+                    v[0] = fmaf(t.y, fmaf(-t.x, c.x, v[0]), b.x);
+                    v[1] = fmaf(t.y, fmaf(-t.x, c.y, v[1]), b.y);
+                    v[2] = fmaf(t.y, fmaf(-t.x, c.z, v[2]), b.z);
+                    v[3] = fmaf(t.y, fmaf(-t.x, c.w, v[3]), b.w);
+                } else {
+                    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+                }
+                if constexpr (ACT == ACT_GELU) {
+                    v = gelu_fast4(v);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(v[e]);
+                }
+                h[r] = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+            }
+            const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
+            const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
+            const u32x4 d = {x[0], y[0], x[1], y[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(d, osrd, voff + j * 32, 0, 0);
+        }
+        voff += 32 * ldo2;
+    }
+}
+
+template <int ACT, int EPI>
+__device__ __forceinline__ void w4_epilogue_bf16(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase, int nbase,
+                                                 int lane, const char* side) {
+    if (nbase >= p.N) return;                                   // wave-uniform
+    if (p.N - nbase >= 128) w4_epilogue_bf16_n<ACT, EPI, 8>(p, acc, mbase, nbase, lane, side);
+    else w4_epilogue_bf16_n<ACT, EPI, 4>(p, acc, mbase, nbase, lane, side);   // N % 128 == 64
+}
+
 // Diagnostic timeline (ce_set_gemm_trace): wave 0 of each workgroup records s_memrealtime (100 MHz,
 // chip-wide) at start, after the K-loop and after its epilogue, plus the hardware id word, into
 // its own buffer (nothing else reads it).  Null in normal runs.
-__device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot_idx) {
-    if (p.trace && threadIdx.x == 0 && blockIdx.x < p.trace_n) {
-        unsigned long long* r = p.trace + (size_t)blockIdx.x * 4;
+__device__ __forceinline__ void trace_stamp(const GemmParams& p, int slot_idx, int rec = -1) {
+    if (rec < 0) rec = blockIdx.x;
+    if (p.trace && threadIdx.x == 0 && rec < p.trace_n) {
+        unsigned long long* r = p.trace + (size_t)rec * 4;
         r[slot_idx] = __builtin_amdgcn_s_memrealtime();
         if (slot_idx == 0) {
             unsigned hw;
@@ -1188,12 +1301,14 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4p(GemmParams p) {
 // tiles a workgroup owns (grid = one workgroup per CU; tile r*grid + xcd_remap(b) in round r).
 // The DMA two K-tiles ahead runs into the next tile's first K-tiles, so the next tile's
 // operands are in flight while this tile's epilogue runs and there is no per-tile prologue.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN, int EV = 0>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    constexpr bool SIDE = EV == 1;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + (SIDE ? 4 * W4_SIDE_BYTES : 0)];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char* const side = smem + 2 * STAGE_BYTES + wave * W4_SIDE_BYTES;
     const int wm = wave >> 1, wn = wave & 1;
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tiles_n = (p.N + BN - 1) / BN;
@@ -1203,6 +1318,16 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     const int nk = p.K / BK;
     const int my_tiles = slot < nwg ? (nwg - 1 - slot) / grid + 1 : 0;
     const int nsteps = my_tiles * nk;
+    const bool nowait = (p.variant & GEMM_VAR_W4PP_NOWAIT) != 0;
+    // De-synchronised start (p.stagger, units of s_sleep 16 ~ 1k cycles): equal tiles keep every
+    // CU in lock-step, so all epilogues would store at once and share the HBM write bandwidth
+    // (a 128-KB bf16 tile stores at ~100 GB/s from one CU alone, ~27 GB/s when all 256 store).
+    // Phase k in 1..7 of the CUs that own one tile fewer than the others starts k x stagger late,
+    // which spreads the epilogues over the tile period without lengthening the launch.
+    if (p.stagger > 0 && nwg % grid != 0 && slot >= nwg % grid) {
+        const int ph = 1 + slot % 7;
+        for (int i = 0; i < ph * p.stagger; ++i) __builtin_amdgcn_s_sleep(16);
+    }
 
     const int srow = wave * 8 + (lane >> 3);
     const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
@@ -1274,43 +1399,46 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     // the fragments each MFMA reads.
 #define CE_MFMA_AGPR(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
-    int g = 0;
-    for (int t = 0; t < my_tiles; ++t) {
-        for (int kt = 0; kt < nk; ++kt, ++g) {
-            const int buf = g & 1;
-            const char* sb = smem + buf * STAGE_BYTES;
-            const char* so = smem + (buf ^ 1) * STAGE_BYTES;
-            // ---- B1: MFMA(set0, rows 0-3), set1 of this K-tile read under it (one per 2 MFMAs) ----
+    // first K-tile of a tile (EV 1): C = 0 instead of zeroing 256 accumulators per tile
+#define CE_MFMA_AGPR0(ACC, BV, AV) \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(BV), "v"(AV))
+    constexpr bool NEWLOOP = EV == 1;
+    // K-tile phases.  ZERO: first K-tile of a tile (C = 0 on each accumulator's first MFMA).
+    // B3's PRE: read set0 of the next K-tile under its MFMAs; with EV 1 the last K-tile of a tile
+    // does not (the next tile's set0 is read after the epilogue, so the epilogue has those 64
+    // VGPRs), reading it after the epilogue instead (read_set0).
+    auto B1 = [&](const char* sb, auto zero) __attribute__((always_inline)) {
 #pragma unroll
-            for (int s2 = 0; s2 < 32; ++s2) {
-                const int i = s2 >> 3, j = s2 & 7;
-                CE_MFMA_AGPR(acc[i][j], b0[j], a0[i]);
-                if (s2 & 1) {
-                    const int q = s2 >> 1;      // 0..15: b1[0..7], a1[0..7]
-                    if (q < 8) b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
-                    else a1[q - 8] = *reinterpret_cast<const bf16x8*>(sb + a_off + (q - 8) * 16 * 128 + fo1);
-                }
+        for (int s2 = 0; s2 < 32; ++s2) {
+            const int i = s2 >> 3, j = s2 & 7;
+            if constexpr (decltype(zero)::value) CE_MFMA_AGPR0(acc[i][j], b0[j], a0[i]);
+            else CE_MFMA_AGPR(acc[i][j], b0[j], a0[i]);
+            if (s2 & 1) {
+                const int q = s2 >> 1;      // 0..15: b1[0..7], a1[0..7]
+                if (q < 8) b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
+                else a1[q - 8] = *reinterpret_cast<const bf16x8*>(sb + a_off + (q - 8) * 16 * 128 + fo1);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            barrier();
-            // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); DMA of step g+2 (one per 4) ----
-            const bool live = g + 2 < nsteps;
+        }
+    };
+    auto B2 = [&](int buf, bool live, auto zero) __attribute__((always_inline)) {
 #pragma unroll
-            for (int s2 = 0; s2 < 64; ++s2) {
-                const int i = (s2 >> 3) & 3, j = s2 & 7;
-                if (s2 < 32) CE_MFMA_AGPR(acc[4 + i][j], b0[j], a0[4 + i]);
-                else CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
-                if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
+        for (int s2 = 0; s2 < 64; ++s2) {
+            const int i = (s2 >> 3) & 3, j = s2 & 7;
+            if (s2 < 32) {
+                if constexpr (decltype(zero)::value) CE_MFMA_AGPR0(acc[4 + i][j], b0[j], a0[4 + i]);
+                else CE_MFMA_AGPR(acc[4 + i][j], b0[j], a0[4 + i]);
+            } else {
+                CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
             }
-            advance();
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            barrier();
-            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it (the last K-tile's
-            // reads fetch the next tile's K-tile 0) ----
+            if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
+        }
+    };
+    auto B3 = [&](const char* so, auto pre) __attribute__((always_inline)) {
 #pragma unroll
-            for (int s2 = 0; s2 < 32; ++s2) {
-                const int i = s2 >> 3, j = s2 & 7;
-                CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+        for (int s2 = 0; s2 < 32; ++s2) {
+            const int i = s2 >> 3, j = s2 & 7;
+            CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+            if constexpr (decltype(pre)::value) {
                 if (s2 & 1) {
                     const int q = s2 >> 1;      // a0[0], b0[0..7], a0[1..7]
                     if (q == 0) a0[0] = *reinterpret_cast<const bf16x8*>(so + a_off + fo0);
@@ -1319,8 +1447,60 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
                 }
             }
         }
+    };
+    auto read_set0 = [&](const char* so) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            b0[q] = *reinterpret_cast<const bf16x8*>(so + w_off + q * 16 * 128 + fo0);
+            a0[q] = *reinterpret_cast<const bf16x8*>(so + a_off + q * 16 * 128 + fo0);
+        }
+    };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    int g = 0;
+    for (int t = 0; t < my_tiles; ++t) {
         int tm, tn;
         tile_of(slot + t * grid, tiles_m, tiles_n, p.gm, tm, tn);
+        trace_stamp(p, 0, t * grid + blockIdx.x);     // diagnostics: one record per tile
+        // one K-tile: B1 | barrier | B2 + DMA(step g+2) | wait + barrier | B3
+        auto ktile = [&](int kt, auto pre) __attribute__((always_inline)) {
+            // epilogue operands of this tile into the side area; retired by this K-tile's B2 wait
+            if (SIDE && kt == nk - 1) w4_side_fill<EPI>(p, side, tm * BM + wm * 128, tn * BN + wn * 128, lane);
+            const int buf = g & 1;
+            const char* sb = smem + buf * STAGE_BYTES;
+            const char* so = smem + (buf ^ 1) * STAGE_BYTES;
+            // ---- B1: MFMA(set0, rows 0-3), set1 of this K-tile read under it (one per 2 MFMAs) ----
+            B1(sb, F_{});
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier();
+            // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); DMA of step g+2 (one per 4) ----
+            B2(buf, g + 2 < nsteps, F_{});
+            advance();
+            // K-tile g+1 landed.  Right after an epilogue (kt == 0 of a later tile) it already has:
+            // the epilogue began with vmcnt(0) and B1 ended with a barrier.  Waiting here would also
+            // drain every store of that epilogue (vmcnt retires loads, DMAs and stores in issue
+            // order), exposing their write latency; skipped, they drain under this tile's MFMAs.
+            if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            barrier();
+            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it ----
+            B3(so, pre);
+            ++g;
+        };
+        if constexpr (NEWLOOP) {
+            // the last K-tile does not read the next tile's set0 (read after the epilogue, which
+            // then has those 64 VGPRs)
+            for (int kt = 0; kt < nk - 1; ++kt) ktile(kt, T_{});
+            ktile(nk - 1, F_{});
+        } else {
+            for (int kt = 0; kt < nk; ++kt) ktile(kt, T_{});
+        }
+        trace_stamp(p, 1, t * grid + blockIdx.x);
+        // the next tile's K-tile 1 (DMA issued in this tile's last B2) retires before any epilogue
+        // load or store is issued (see the B2 wait above)
+        if (nowait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (SIDE && OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) {
+            w4_epilogue_bf16<ACT, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
+        } else {
 #if CE_W4_EPI_HALVES
         // the 128-column quadrant as two 64-column epilogues: the NJ = 4 path (4-deep residual
         // ring, a quarter of the live epilogue registers)
@@ -1338,11 +1518,17 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8, CE_RESID_RING, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128,
                                                                      lane);
 #endif
+        }
+        trace_stamp(p, 2, t * grid + blockIdx.x);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // set0 of the next tile's first K-tile (step g; its DMA was retired before the epilogue
+        // and published by the last B2 barrier; its buffer is not refilled before that K-tile's B2)
+        if constexpr (NEWLOOP) read_set0(smem + (g & 1) * STAGE_BYTES);
     }
+#undef CE_MFMA_AGPR0
 #undef CE_MFMA_AGPR
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -1502,6 +1688,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_w2(GemmParams p) {
     trace_stamp(p, 2);
 }
 
+int g_variant = -1;
+int gemm_variant() {
+    if (g_variant < 0) {
+        const char* e = getenv("CE_GEMM_VARIANT");
+        g_variant = e ? std::max(0, atoi(e)) : CE_GEMM_VAR_DEFAULT;
+    }
+    return g_variant;
+}
+
 int g_sched = -1;
 int g_ring = CE_RESID_RING;     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
 unsigned long long* g_trace = nullptr;
@@ -1597,6 +1792,13 @@ float* kernel_api_part() {
     return g_part[dev];
 }
 
+// the four-wave epilogue written for one wave per SIMD (bf16 out, no residual)
+template <bool HAS_RESID, bool OUT_BF16, int EPI>
+bool w4_epi2(const GemmParams& p) {
+    if constexpr (OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) return (p.variant & GEMM_VAR_W4_EPI2) != 0;
+    else return false;
+}
+
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
 int w4pp_grid(int nwg) {
     int grid = (num_cus() / 8) * 8;
@@ -1672,8 +1874,12 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     if (gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     if (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID)) {
         p.gm = gemm_groupm();
+        p.stagger = gemm_stagger();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
         count_path(GEMM_PATH_W4PP + EPI);
         return hipGetLastError();
     }
@@ -1725,7 +1931,12 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         grid = grid < need ? grid : need;
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
     } else if (sc == 11) {
-        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+        p.stagger = gemm_stagger();
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(w4pp_grid(nwg)), dim3(256), 0,
+                               s, p);
+        else
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
     } else if (sc == 10)
         hipLaunchKernelGGL((gemm_bf16_w4p<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
     else if (sc == 2)
@@ -1754,6 +1965,12 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
 }
 
 }  // namespace
+
+int set_gemm_variant(int bits) {
+    const int prev = gemm_variant();
+    g_variant = bits >= 0 ? bits : CE_GEMM_VAR_DEFAULT;
+    return prev;
+}
 
 int set_gemm_auto(int mode) {
     const int prev = gemm_auto();
@@ -1799,6 +2016,7 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     GemmParams p = p0;
     p.trace = g_trace;
     p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
+    p.variant = gemm_variant();
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;

@@ -264,6 +264,10 @@ int ce_set_gemm_splitk(int enable);
  * 2 = every large grid on it, 3 = large grids without a residual.  Returns the previous mode.
  * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
 int ce_set_gemm_auto(int mode);
+/* GEMM kernel-variant bits for A/B measurement (env CE_GEMM_VARIANT at first use; a negative value
+ * restores the default): bit 0 = the four-wave persistent schedule does not drain an epilogue's
+ * stores at the next tile's first K-tile (default on).  Returns the previous bits. */
+int ce_set_gemm_variant(int bits);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
  * schedules, 10 = two-workgroup 256 x 128 (SCHED 12), and epi 0 = plain, 1 = LN statistics, 2 = LN

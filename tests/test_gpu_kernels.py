@@ -91,6 +91,70 @@ def test_gemm_splitk_tail(M, N, K, variant):
     assert (outs[0] - outs[1]).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("M,N,K", [(33280, 1024, 1024), (20000, 3072, 1024), (17000, 1024, 4096)])
+@pytest.mark.parametrize("variant", ["gelu_bf16", "resid_f32", "bias_bf16"])
+@pytest.mark.parametrize("bits", [0, 1, 3])
+def test_gemm_persistent_multitile(M, N, K, variant, bits):
+    """The four-wave persistent schedule (SCHED 11) with several tiles per workgroup, so the
+    epilogue -> next-tile hand-over (and its variant bits) runs; vs the f32 reference."""
+    L = _lib.lib()
+    prev, prev_v = L.ce_set_gemm_schedule(11), L.ce_set_gemm_variant(bits)
+    try:
+        g = torch.Generator(device="cpu").manual_seed(M + N + K + bits)
+        A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+        W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+        bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+        resid = torch.randn(M, N, generator=g).to(DEV) if variant == "resid_f32" else None
+        act = 1 if variant == "gelu_bf16" else 0
+        out_bf16 = variant.endswith("bf16")
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+        _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), act, P(resid), P(out),
+                  _lib.CE_BF16 if out_bf16 else _lib.CE_F32)
+        torch.cuda.synchronize()
+    finally:
+        L.ce_set_gemm_schedule(prev)
+        L.ce_set_gemm_variant(prev_v)
+    ref = gemm_ref(A, W, bias, act, resid)
+    err = (out.float() - ref).abs().max().item()
+    tol = (8e-3 if out_bf16 else 2e-4) * ref.abs().max().item() + 1e-5
+    assert err <= tol, f"max err {err} vs tol {tol}"
+
+
+@pytest.mark.parametrize("M,N,act", [(20000, 3072, 0), (20000, 4096, 1), (20000, 4096, 2), (300, 1024, 1)])
+@pytest.mark.parametrize("bits", [1, 3])
+def test_gemm_persistent_ln_fold(M, N, act, bits):
+    """SCHED 11 with the LN-fold epilogue (QKV / c_fc of the folded image tower), both epilogue
+    versions (bit 1: operands staged in LDS by DMA, buffer stores clipped at row M):
+    out = act(rstd_m (A W^T - mu_m c_n) + d_n) vs torch f32; M % 256 != 0 exercises the row clip."""
+    K = 1024
+    L = _lib.lib()
+    g = torch.Generator(device="cpu").manual_seed(M + N + act + bits)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    mu = (torch.randn(M, generator=g) * 0.2).to(DEV)
+    rstd = (torch.rand(M, generator=g) * 1.5 + 0.5).to(DEV)
+    stats = torch.stack([mu, rstd], 1).contiguous()
+    fold_c = W.float().sum(1).contiguous()
+    out = torch.full((M + 64, N), 7.0, device=DEV, dtype=torch.bfloat16)   # rows >= M must stay untouched
+    prev, prev_v = L.ce_set_gemm_schedule(11), L.ce_set_gemm_variant(bits)
+    try:
+        _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), act, None, P(out), _lib.CE_BF16,
+                  2, None, None, P(stats), P(fold_c))
+        torch.cuda.synchronize()
+    finally:
+        L.ce_set_gemm_schedule(prev)
+        L.ce_set_gemm_variant(prev_v)
+    ref = rstd[:, None] * (A.float() @ W.float().t() - mu[:, None] * fold_c[None, :]) + bias
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    elif act == 2:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    err = (out[:M].float() - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item() + 1e-5, err
+    assert bool((out[M:] == 7.0).all())
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     n = 256

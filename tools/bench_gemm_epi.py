@@ -3,7 +3,7 @@
 (guide §5.4 rule 24), random data.
 
     python tools/bench_gemm_epi.py --scheds 1,12 [--rounds 3] [--reps 10] [--only fc,qkv]
-A schedule token: <sched>[g<groupm>][a<auto>][s<stagger>][n]  (n: split-K tail off; a0: auto policy off;\ns<k>: first-round stagger of k x s_sleep 127 for half the CUs).
+A schedule token: <sched>[g<groupm>][a<auto>][s<stagger>][v<variant bits>][n]  (n: split-K tail off; a0: auto policy off;\ns<k>: first-round stagger of k x s_sleep 127 for half the CUs).
 """
 import argparse
 import ctypes
@@ -38,18 +38,15 @@ def timeit(fn, reps):
 
 
 def parse(tok):
-    split = 0 if tok.endswith("n") else 1
-    tok = tok.rstrip("n")
-    auto = 1
-    stag = 0
-    if "s" in tok:
-        tok, _, st = tok.partition("s")
-        stag = int(st) + 1
-    if "a" in tok:
-        tok, _, a = tok.partition("a")
-        auto = int(a)
-    sc, _, gm = tok.partition("g")
-    return int(sc), int(gm or 0), auto, split, stag
+    """<sched>[g<groupm>][a<auto>][s<stagger>][v<variant bits>][n], modifiers in any order."""
+    import re
+    m = re.fullmatch(r"(\d+)((?:[gasv]\d+)*)(n?)", tok)
+    if not m:
+        raise ValueError(f"bad schedule token {tok!r}")
+    mods = {k: int(v) for k, v in re.findall(r"([gasv])(\d+)", m.group(2))}
+    split = 0 if m.group(3) else 1
+    stag = mods.get("s", 0) + 1          # always explicit (0 would keep the previous value)
+    return int(m.group(1)), mods.get("g", 0), mods.get("a", 1), split, stag, mods.get("v", -1)
 
 
 def main():
@@ -65,7 +62,7 @@ def main():
     # name: (N, K, act, epi, resid, out_bf16)
     shapes = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True, False),
               "fc": (4096, 1024, 1, 2, False, True), "proj": (1024, 4096, 0, 1, True, False),
-              "fc_plain": (4096, 1024, 0, 0, False, True), "sq": (4096, 4096, 0, 0, False, True)}
+              "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True), "sq": (4096, 4096, 0, 0, False, True)}
     if args.only:
         shapes = {k: v for k, v in shapes.items() if k in args.only.split(",")}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -95,7 +92,8 @@ def main():
     L = _lib.lib()
     for _ in range(args.rounds):
         for tok in args.scheds.split(","):
-            sc, gm, auto, split, stag = parse(tok)
+            sc, gm, auto, split, stag, var = parse(tok)
+            L.ce_set_gemm_variant(var)
             L.ce_set_gemm_schedule(sc | (gm << 8) | (stag << 24))
             L.ce_set_gemm_auto(auto)
             L.ce_set_gemm_splitk(split)

@@ -1,4 +1,4 @@
-"""Per-workgroup timeline of a GEMM launch (ce_set_gemm_trace, s_memrealtime at 100 MHz):
+"""Per-workgroup (per-tile for the persistent SCHED 11) timeline of a GEMM launch (ce_set_gemm_trace, s_memrealtime at 100 MHz):
 K-loop and epilogue durations and how many workgroups are in their epilogue at once.
 
     python tools/gemm_trace.py --shape out --scheds 1,1s4,12
@@ -19,7 +19,7 @@ from bench_gemm_epi import P, parse  # noqa: E402
 
 SHAPES = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True, False),
           "fc": (4096, 1024, 1, 2, False, True), "proj": (1024, 4096, 0, 1, True, False),
-          "fc_plain": (4096, 1024, 0, 0, False, True)}
+          "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True)}
 
 
 def main():
@@ -51,7 +51,8 @@ def main():
                   _lib.CE_BF16 if ob else _lib.CE_F32, epi, P(xb), P(part), P(st), P(fc))
 
     for tok in args.scheds.split(","):
-        sc, gm, auto, split, stag = parse(tok)
+        sc, gm, auto, split, stag, var = parse(tok)
+        L.ce_set_gemm_variant(var)
         L.ce_set_gemm_schedule(sc | (gm << 8) | (stag << 24))
         L.ce_set_gemm_auto(auto)
         L.ce_set_gemm_splitk(split)
