@@ -112,9 +112,14 @@ struct FoldOps {
 #endif
 
 // kernel-variant bits (set_gemm_variant / env CE_GEMM_VARIANT), default GEMM_VAR_DEFAULT
-enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2 };
+enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
+       // timing ablations of the four-wave LN-stats epilogue (wrong outputs; micro-benchmarks only)
+       GEMM_VAR_ABL_NORESID = 4, GEMM_VAR_ABL_NOSTORE = 8,
+       // the four-wave schedule with one tile per workgroup (grid = tiles): an exiting workgroup's
+       // stores drain while the next one on the CU starts, instead of ahead of the next tile's DMAs
+       GEMM_VAR_W4_ONETILE = 16 };
 #ifndef CE_GEMM_VAR_DEFAULT
-#define CE_GEMM_VAR_DEFAULT GEMM_VAR_W4PP_NOWAIT
+#define CE_GEMM_VAR_DEFAULT (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2)
 #endif
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
@@ -409,6 +414,119 @@ __device__ __forceinline__ void w4_epilogue_bf16(const GemmParams& p, const f32x
     if (nbase >= p.N) return;                                   // wave-uniform
     if (p.N - nbase >= 128) w4_epilogue_bf16_n<ACT, EPI, 8>(p, acc, mbase, nbase, lane, side);
     else w4_epilogue_bf16_n<ACT, EPI, 4>(p, acc, mbase, nbase, lane, side);   // N % 128 == 64
+}
+
+// Four-wave epilogue of the residual GEMMs with LN statistics (out-proj / c_proj of the folded image
+// tower, EPI_LN_STATS): out f32 = acc + bias + resid, xb = bf16(out), per-64-column-slab (mean, M2)
+// of every row.  The residual rows are prefetched RD - 1 fragment rows ahead through a buffer
+// descriptor clipped at row M (rows past M read zeros; their outputs are dropped the same way), so
+// each residual wait is for loads issued before the previous rows' stores.
+template <int JN, int RD, int NJA>
+__device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 (&acc)[8][NJA], int mbase, int nbase,
+                                               int lane, const float4 (&bv)[JN]) {
+    constexpr int NS = JN / 4;                                  // 64-column slabs of the quadrant
+    const int fr = lane & 15, fq = lane >> 4;
+    const int rows = max(0, min(p.M - mbase, 128));
+    const int ldo = (int)p.ldo, ldr = (int)p.ldr;
+    // one descriptor per buffer over the quadrant's rows [mbase, M); lane offsets advance by one
+    // fragment row (16 rows) per step, the 16-column step is the immediate
+    const __amdgpu_buffer_rsrc_t os = make_srd(static_cast<float*>(p.out) + (size_t)mbase * ldo, rows * ldo * 4);
+    const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
+    const __amdgpu_buffer_rsrc_t rs = make_srd(p.resid + (size_t)mbase * ldr, rows * ldr * 4);
+    int ooff = (fr * ldo + nbase + fq * 4) * 4;                                    // + j*64
+    int roff = (fr * ldr + nbase + fq * 4) * 4;
+    int xoff = ((fr + (fq & 1) * 16) * ldo + nbase + (fq >> 1) * 8) * 2;           // row pair, + j*32
+    const int ostep = 16 * ldo * 4, rstep = 16 * ldr * 4, xstep = 32 * ldo * 2;
+    f32x4 rv[RD][JN];
+    const bool abl_r = (p.variant & GEMM_VAR_ABL_NORESID) != 0, abl_s = (p.variant & GEMM_VAR_ABL_NOSTORE) != 0;
+    auto load_r = [&](f32x4 (&r)[JN]) {     // the next fragment row's residual
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+            r[j] = abl_r ? f32x4{0.f, 0.f, 0.f, 0.f}
+                         : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, roff + j * 64, 0, 0));
+        roff += rstep;
+    };
+#pragma unroll
+    for (int i = 0; i < RD - 1; ++i) load_r(rv[i]);
+    uint2 pxb[JN];
+    float2 sta[NS], stb[NS];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (i + RD - 1 < 8) load_r(rv[(i + RD - 1) % RD]);
+        float lmean[NS], lm2[NS];
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+            f32x4 v = acc[i][j];
+            const f32x4 r = rv[i % RD][j];
+            v[0] += bv[j].x + r[0]; v[1] += bv[j].y + r[1]; v[2] += bv[j].z + r[2]; v[3] += bv[j].w + r[3];
+            if (!abl_s) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), os, ooff + j * 64, 0, 0);
+            // Chan's pairwise update: the 4 values of block j join the lane's 4jj earlier ones
+            const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+            const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
+            const float q4 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
+            const int sl = j >> 2, jj = j & 3;
+            if (jj == 0) {
+                lmean[sl] = m4;
+                lm2[sl] = q4;
+            } else {
+                const float dl = m4 - lmean[sl];
+                lmean[sl] = fmaf(dl, 1.0f / (jj + 1), lmean[sl]);
+                lm2[sl] += fmaf(dl * dl, 4.0f * jj / (jj + 1), q4);
+            }
+            const uint2 o = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+            if ((i & 1) == 0) {
+                pxb[j] = o;
+            } else {
+                const auto x = __builtin_amdgcn_permlane16_swap(pxb[j].x, o.x, false, false);
+                const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
+                const u32x4 d = {x[0], y[0], x[1], y[1]};
+                if (!abl_s) __builtin_amdgcn_raw_buffer_store_b128(d, xs, xoff + j * 32, 0, 0);
+            }
+        }
+        ooff += ostep;
+        if (i & 1) xoff += xstep;
+        // (mean, M2) of this row's 64-column slabs: 4 lanes (fq) of 16 values each, Chan's formula
+        // for equal counts; lane group fq keeps fragment rows fq and fq + 4
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            float sm = lmean[sl];
+            sm += __shfl_xor(sm, 16, 64);
+            sm += __shfl_xor(sm, 32, 64);
+            const float mean = sm * 0.25f;
+            const float dl = lmean[sl] - mean;
+            float q = fmaf(dl * dl, 16.0f, lm2[sl]);
+            q += __shfl_xor(q, 16, 64);
+            q += __shfl_xor(q, 32, 64);
+            if (fq == (i & 3)) {
+                if (i < 4) sta[sl] = make_float2(mean, q);
+                else stb[sl] = make_float2(mean, q);
+            }
+        }
+    }
+    const int ma = mbase + fq * 16 + fr, mb = ma + 64;
+    const size_t ns = p.N / 64;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+        if (ma < p.M) p.stats_part[(size_t)ma * ns + nbase / 64 + sl] = sta[sl];
+        if (mb < p.M) p.stats_part[(size_t)mb * ns + nbase / 64 + sl] = stb[sl];
+    }
+}
+
+template <int JN, int RD>
+__device__ __forceinline__ void w4_epilogue_stats_n(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase, int nbase,
+                                                    int lane, const char* side) {
+    const float4* sb = reinterpret_cast<const float4*>(side) + (lane >> 4);
+    float4 bv[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) bv[j] = sb[4 * j];
+    epi_stats_rows<JN, RD>(p, acc, mbase, nbase, lane, bv);
+}
+
+__device__ __forceinline__ void w4_epilogue_stats(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase, int nbase,
+                                                  int lane, const char* side) {
+    if (nbase >= p.N) return;                                   // wave-uniform
+    if (p.N - nbase >= 128) w4_epilogue_stats_n<8, 2>(p, acc, mbase, nbase, lane, side);
+    else w4_epilogue_stats_n<4, 2>(p, acc, mbase, nbase, lane, side);   // N % 128 == 64
 }
 
 // Diagnostic timeline (ce_set_gemm_trace): wave 0 of each workgroup records s_memrealtime (100 MHz,
@@ -1349,12 +1467,16 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     auto dma = [&](int buf, int j, bool live) {
         const int kb = live ? dk * BK * 2 : 0x7ffff000;
         char* base = smem + buf * STAGE_BYTES;
+        // the row-group offset is made opaque so hipcc forms each DMA's VGPR offset in place
+        // (one v_add) instead of keeping 16 loop-invariant offsets live across the epilogue
+        int jo = (j < 8 ? j : j - 8) * (j < 8 ? jstrA : jstrW);
+        asm volatile("" : "+s"(jo));
         if (j < 8)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + (j * 32 + wave * 8) * 128), 16,
-                                                     voffA + j * jstrA, kb, 0, 0);
+                                                     voffA + jo, kb, 0, 0);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + TILE_BYTES + ((j - 8) * 32 + wave * 8) * 128),
-                                                     16, voffW + (j - 8) * jstrW, kb, 0, 0);
+                                                     16, voffW + jo, kb, 0, 0);
     };
     auto advance = [&] {
         if (++dk == nk) {
@@ -1500,6 +1622,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         if (nowait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (SIDE && OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) {
             w4_epilogue_bf16<ACT, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
+        } else if constexpr (SIDE && EPI == EPI_LN_STATS) {
+            w4_epilogue_stats(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
         } else {
 #if CE_W4_EPI_HALVES
         // the 128-column quadrant as two 64-column epilogues: the NJ = 4 path (4-deep residual
@@ -1796,22 +1920,27 @@ float* kernel_api_part() {
 template <bool HAS_RESID, bool OUT_BF16, int EPI>
 bool w4_epi2(const GemmParams& p) {
     if constexpr (OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) return (p.variant & GEMM_VAR_W4_EPI2) != 0;
+    else if constexpr (EPI == EPI_LN_STATS) return (p.variant & GEMM_VAR_W4_EPI2) != 0 && p.grp == 0;
     else return false;
 }
 
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
+// (GEMM_VAR_W4_ONETILE: one workgroup per tile)
 int w4pp_grid(int nwg) {
-    int grid = (num_cus() / 8) * 8;
     const int need = ((nwg + 7) / 8) * 8;
+    if (gemm_variant() & GEMM_VAR_W4_ONETILE) return need;
+    const int grid = (num_cus() / 8) * 8;
     return grid < need ? grid : need;
 }
 
-// Shape policy of the default schedule (CE_GEMM_AUTO, default 1): SCHED 11 for large grids with
-// no activation and no residual — the vision QKV GEMM, plain or LN-folded (in-model 20.3 vs 23.1
-// ms/step).  Epilogues with GELU or a residual stay on SCHED 1: one wave per SIMD pays them
-// serially (c_fc + fold + GELU 35.9 vs 34.4, c_proj + stats 30.0 vs 29.3, out-proj 14.0 vs 12.8;
-// profiles/r01_gemm_w4p_sched10_11.log).  CE_GEMM_AUTO=0 pins SCHED 1, =2 sends every large
-// grid to SCHED 11.  Only for grids of >= 4 tiles per CU.
+// Shape policy of the default schedule (CE_GEMM_AUTO, default 1): SCHED 11 for large grids
+// (>= 4 tiles per CU) without a residual — the vision QKV and c_fc GEMMs, plain or LN-folded, with
+// or without GELU — when its one-wave-per-SIMD epilogue (GEMM_VAR_W4_EPI2) is on; otherwise only
+// the no-activation ones (the round-1 policy).  Residual epilogues (out-proj / c_proj) stay on
+// SCHED 1: on the persistent grid vmcnt retires the epilogue's stores and the next tile's DMAs in
+// issue order, so their 384 KB per tile must drain within two K-tiles (r02 A/B: out-proj 572 vs
+// 593 TF/s, c_proj 1037 vs 1025; with the stores ablated 855 / 1204, profiles/r02).
+// CE_GEMM_AUTO=0 pins SCHED 1, =2 sends every large grid to SCHED 11, =3 every residual-free one.
 int g_auto = -1;
 int gemm_auto() {
     if (g_auto < 0) {
@@ -1830,7 +1959,8 @@ bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     if (nwg < 4 * num_cus()) return false;
     if (on == 2) return true;
     if (on == 3) return !resid;
-    return act == ACT_NONE && !resid;
+    if (resid) return false;
+    return act == ACT_NONE || (gemm_variant() & GEMM_VAR_W4_EPI2) != 0;
 }
 
 // Launch counters per kernel path (ce_gemm_path_counts): lets the parity tests assert that the

@@ -260,13 +260,16 @@ int ce_set_gemm_schedule(int schedule);
 int ce_set_gemm_splitk(int enable);
 /* Shape policy of the default GEMM schedule (env CE_GEMM_AUTO at first use): 0 = every GEMM on
  * the 4-phase schedule (with its split-K tail), 1 = the default (grids of >= 4 tiles per CU with
- * no activation and no residual, i.e. the vision QKV GEMM, on the four-wave persistent schedule),
+ * no residual, i.e. the vision QKV and c_fc GEMMs, on the four-wave persistent schedule),
  * 2 = every large grid on it, 3 = large grids without a residual.  Returns the previous mode.
  * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
 int ce_set_gemm_auto(int mode);
 /* GEMM kernel-variant bits for A/B measurement (env CE_GEMM_VARIANT at first use; a negative value
- * restores the default): bit 0 = the four-wave persistent schedule does not drain an epilogue's
- * stores at the next tile's first K-tile (default on).  Returns the previous bits. */
+ * restores the default, bits 0|1): bit 0 = the four-wave persistent schedule does not drain an
+ * epilogue's stores at the next tile's first K-tile; bit 1 = its epilogue written for one wave per
+ * SIMD (operands staged in LDS, clipped buffer stores; also lets the default policy put GELU GEMMs on
+ * that schedule); bits 2, 3 = timing ablations of its LN-statistics epilogue (no residual loads /
+ * no stores: wrong outputs).  Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other

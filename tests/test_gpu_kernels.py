@@ -155,6 +155,43 @@ def test_gemm_persistent_ln_fold(M, N, act, bits):
     assert bool((out[M:] == 7.0).all())
 
 
+@pytest.mark.parametrize("M,K", [(20000, 1024), (9000, 4096), (300, 1024)])
+@pytest.mark.parametrize("bits", [1, 3])
+def test_gemm_persistent_ln_stats(M, K, bits):
+    """SCHED 11 with the LN-statistics epilogue (out-proj / c_proj of the folded image tower), both
+    epilogue versions: out f32 = A W^T + bias + resid, xb = bf16(out), per-64-column (mean, M2)
+    slab statistics, vs torch f32; rows >= M of every output stay untouched."""
+    N = 1024
+    L = _lib.lib()
+    g = torch.Generator(device="cpu").manual_seed(M + K + bits)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    resid = torch.randn(M, N, generator=g).to(DEV)
+    ns = N // 64
+    out = torch.full((M + 32, N), 7.0, device=DEV)
+    xb = torch.full((M + 32, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    part = torch.full((M + 32, ns, 2), 7.0, device=DEV)
+    prev, prev_v = L.ce_set_gemm_schedule(11), L.ce_set_gemm_variant(bits)
+    try:
+        _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(resid), P(out), _lib.CE_F32,
+                  1, P(xb), P(part), None, None)
+        torch.cuda.synchronize()
+    finally:
+        L.ce_set_gemm_schedule(prev)
+        L.ce_set_gemm_variant(prev_v)
+    ref = A.float() @ W.float().t() + bias + resid
+    scale = ref.abs().max().item()
+    assert (out[:M] - ref).abs().max().item() <= 2e-4 * scale + 1e-5
+    assert (xb[:M].float() - ref).abs().max().item() <= 8e-3 * scale
+    r3 = ref.reshape(M, ns, 64)
+    mean = r3.mean(-1)
+    m2 = ((r3 - mean[..., None]) ** 2).sum(-1)
+    assert (part[:M, :, 0] - mean).abs().max().item() <= 1e-4 * scale
+    assert (part[:M, :, 1] - m2).abs().max().item() <= 1e-4 * m2.abs().max().item() + 1e-4
+    assert bool((out[M:] == 7.0).all()) and bool((xb[M:] == 7.0).all()) and bool((part[M:] == 7.0).all())
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     n = 256

@@ -8,5 +8,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
   > gpurun_out/${TAG}_pytest.log 2>&1 && echo "pytest ok" && tail -1 gpurun_out/${TAG}_pytest.log &&
 timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 && echo "bench ok" &&
 tail -1 gpurun_out/${TAG}_bench.log &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
   python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 && echo "prof ok"
