@@ -89,21 +89,23 @@ __device__ __forceinline__ f32x2 gelu_pair(f32x2 x) {
     return x * phi;
 }
 
-// GELU as x * sigmoid(z(x)) with z(x) = u * P(u^2), u = clamp(x, +-5), P a degree-4 fit of
+// GELU as x * sigmoid(z(x)) with z(x) = u * P(u^2), u = clamp(x, +-4.75), P a degree-2 fit of
 // logit(Phi) (times -log2 e, so the exponential is one v_exp_f32):  y = x / (1 + 2^(u * P(u^2))).
-// Error <= 9.5e-6 * max(1, |y|) vs the exact-erf GELU over all x in f32 (tests/test_host.py),
-// far below the bf16 rounding of the GEMM output it feeds.  9 VALU + 2 transcendental ops
-// (~52 issue cycles per value for one wave on a SIMD) vs 17 for the degree-12 polynomial above.
-// four independent values per call, so the dependent polynomial chains interleave
+// Error <= 6.2e-5 * max(1, |y|) vs the exact-erf GELU over all x in f32 (tests/test_host.py), 30x
+// below the bf16 rounding (2^-9) of the GEMM output it feeds.  7 VALU + 2 transcendental ops (~44
+// issue cycles per value for one wave on a SIMD) vs 17 VALU for the degree-12 polynomial above.
+#define CE_GELU_CLAMP 4.75f
+#define CE_GELU_C0 -2.29998779296875f
+#define CE_GELU_C1 -0.10797221958637238f
+#define CE_GELU_C2 0.0012323867995291948f
+// four independent values per call, so the dependent chains interleave
 __device__ __forceinline__ f32x4 gelu_fast4(f32x4 x) {
     f32x4 u;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) u[e] = __builtin_amdgcn_fmed3f(x[e], -5.0f, 5.0f);
+    for (int e = 0; e < 4; ++e) u[e] = __builtin_amdgcn_fmed3f(x[e], -CE_GELU_CLAMP, CE_GELU_CLAMP);
     const f32x4 u2 = u * u;
-    f32x4 p = __builtin_elementwise_fma(u2, (f32x4)(-4.781674761034083e-06f), (f32x4)(0.00011614440882112831f));
-    p = __builtin_elementwise_fma(p, u2, (f32x4)(0.00021269964054226875f));
-    p = __builtin_elementwise_fma(p, u2, (f32x4)(-0.10495619475841522f));
-    p = __builtin_elementwise_fma(p, u2, (f32x4)(-2.3021795749664307f));
+    f32x4 p = __builtin_elementwise_fma(u2, (f32x4)(CE_GELU_C2), (f32x4)(CE_GELU_C1));
+    p = __builtin_elementwise_fma(p, u2, (f32x4)(CE_GELU_C0));
     const f32x4 z = u * p;
     f32x4 y;
 #pragma unroll
@@ -111,14 +113,10 @@ __device__ __forceinline__ f32x4 gelu_fast4(f32x4 x) {
     return y;
 }
 __device__ __forceinline__ float gelu_fast(float x) {
-    const float u = __builtin_amdgcn_fmed3f(x, -5.0f, 5.0f);
+    const float u = __builtin_amdgcn_fmed3f(x, -CE_GELU_CLAMP, CE_GELU_CLAMP);
     const float u2 = u * u;
-    float p = fmaf(u2, -4.781674761034083e-06f, 0.00011614440882112831f);
-    p = fmaf(p, u2, 0.00021269964054226875f);
-    p = fmaf(p, u2, -0.10495619475841522f);
-    p = fmaf(p, u2, -2.3021795749664307f);
-    const float e = __builtin_amdgcn_exp2f(u * p);
-    return x * __builtin_amdgcn_rcpf(1.0f + e);
+    const float p = fmaf(fmaf(u2, CE_GELU_C2, CE_GELU_C1), u2, CE_GELU_C0);
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * p));
 }
 
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2 };

@@ -26,6 +26,7 @@ struct GemmParams {
     // (partial f32 tiles into `part`), summed in fixed order by a fixup kernel
     float* part = nullptr; long part_elems = 0;
     int tail = 0, split = 1;
+    int tail_only = 0;                     // 4-phase kernel: run only the split-K chunks (SCHED 11's tail)
     // LayerNorm folded into the GEMMs around it (EPI_LN_STATS / EPI_LN_FOLD):
     //   producer (residual GEMM, f32 out): also xb[m][n] = bf16(out) and, per 64-column slab,
     //     stats_part[m][n/64] = (mean, sum of squared deviations) of the outputs

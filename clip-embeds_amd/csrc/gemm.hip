@@ -117,7 +117,11 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        GEMM_VAR_ABL_NORESID = 4, GEMM_VAR_ABL_NOSTORE = 8,
        // the four-wave schedule with one tile per workgroup (grid = tiles): an exiting workgroup's
        // stores drain while the next one on the CU starts, instead of ahead of the next tile's DMAs
-       GEMM_VAR_W4_ONETILE = 16 };
+       GEMM_VAR_W4_ONETILE = 16,
+       // split-K tail on the four-wave persistent schedule (a last round of <= 1/8 of the grid)
+       GEMM_VAR_W4_TAIL = 32,
+       // timing ablation of the LN-statistics epilogues: no bf16 copy of the output (wrong xb)
+       GEMM_VAR_ABL_NOXB = 64 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2)
 #endif
@@ -255,7 +259,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                         const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
                         const int mrow = (fq & 1) ? m : m - 16;
                         const size_t ob = (size_t)mrow * p.ldo + nbase + (fq & ~1) * 4 + j * 16;
-                        if (!CHECK_M || mrow < p.M)
+                        if ((!CHECK_M || mrow < p.M) && !(p.variant & GEMM_VAR_ABL_NOXB))
                             *reinterpret_cast<uint4*>(p.xb + ob) = make_uint4(x[0], y[0], x[1], y[1]);
                     }
                 }
@@ -878,12 +882,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int tiles_m = (p.M + BM - 1) / BM;
     const int tiles_n = (p.N + BN - 1) / BN;
     const int nwg = tiles_m * tiles_n;
-    const int bid = blockIdx.x;
+    int bid = blockIdx.x;
     const int nk = p.K / BK;
     // split-K tail (SCHED 1): blocks past t_main (dispatched last, so they fill the final, otherwise
     // mostly idle round of the grid) each take one K-chunk of one of the last `tail` tiles
     const int t_main = nwg - (SCHED == 1 ? p.tail : 0);
     int wgid, kt0 = 0, kt1 = nk, slab = -1;
+    if (SCHED == 1 && p.tail_only) bid += t_main;      // only the split-K chunks (SCHED 11's tail)
     if (bid < t_main) {
         wgid = xcd_remap(bid, t_main);
     } else {
@@ -1434,7 +1439,10 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     const int grid = gridDim.x;
     const int slot = xcd_remap(blockIdx.x, grid);
     const int nk = p.K / BK;
-    const int my_tiles = slot < nwg ? (nwg - 1 - slot) / grid + 1 : 0;
+    // whole rounds only when the host planned a split-K tail (its p.tail tiles run as K-chunks on
+    // the 4-phase kernel in tail-only mode, then gemm_splitk_fixup)
+    const int t_main = nwg - p.tail;
+    const int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
     const int nsteps = my_tiles * nk;
     const bool nowait = (p.variant & GEMM_VAR_W4PP_NOWAIT) != 0;
     // De-synchronised start (p.stagger, units of s_sleep 16 ~ 1k cycles): equal tiles keep every
@@ -1442,7 +1450,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     // (a 128-KB bf16 tile stores at ~100 GB/s from one CU alone, ~27 GB/s when all 256 store).
     // Phase k in 1..7 of the CUs that own one tile fewer than the others starts k x stagger late,
     // which spreads the epilogues over the tile period without lengthening the launch.
-    if (p.stagger > 0 && nwg % grid != 0 && slot >= nwg % grid) {
+    if (p.stagger > 0 && p.tail == 0 && nwg % grid != 0 && slot >= nwg % grid) {
         const int ph = 1 + slot % 7;
         for (int i = 0; i < ph * p.stagger; ++i) __builtin_amdgcn_s_sleep(16);
     }
@@ -1924,6 +1932,24 @@ bool w4_epi2(const GemmParams& p) {
     else return false;
 }
 
+// SCHED 11 split-K tail: a grid of nwg tiles over `grid` persistent workgroups whose last round
+// holds r <= grid / 8 tiles idles most of the chip for a whole tile; the persistent kernel runs the
+// whole rounds only, and those r tiles follow as S K-chunks (about 4 K-tiles each, r * S <= grid) on
+// the 4-phase kernel in tail-only mode, summed and finished by gemm_splitk_fixup (vision QKV
+// 6924 = 27 * 256 + 12 tiles, c_fc 9232 = 36 * 256 + 16).
+void plan_tail_w4(GemmParams& p, int nwg, int grid) {
+    p.tail = 0;
+    p.split = 1;
+    if (!splitk_enabled() || !p.part || !(gemm_variant() & GEMM_VAR_W4_TAIL)) return;
+    const int r = nwg % grid, nk = p.K / BK;
+    if (nwg < grid || r == 0 || r > grid / 8) return;
+    int S = std::min(std::min(std::max(nk / 4, 2), 16), std::min(grid / r, nk));
+    while (S >= 2 && (long)r * S * BM * BN > p.part_elems) --S;
+    if (S < 2) return;
+    p.tail = r;
+    p.split = S;
+}
+
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
 // (GEMM_VAR_W4_ONETILE: one workgroup per tile)
 int w4pp_grid(int nwg) {
@@ -2006,11 +2032,21 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         p.gm = gemm_groupm();
         p.stagger = gemm_stagger();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+        const int grid = w4pp_grid(nwg);
+        plan_tail_w4(p, nwg, grid);
         if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(grid), dim3(256), 0, s, p);
         else
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(grid), dim3(256), 0, s, p);
         count_path(GEMM_PATH_W4PP + EPI);
+        if (p.tail > 0) {
+            GemmParams q = p;
+            q.tail_only = 1;
+            hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
+                               dim3(p.tail * p.split), dim3(NTHREADS), 0, s, q);
+            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
+            count_path(GEMM_PATH_FIXUP + EPI);
+        }
         return hipGetLastError();
     }
     p.gm = gemm_groupm();
@@ -2062,11 +2098,19 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
     } else if (sc == 11) {
         p.stagger = gemm_stagger();
+        const int grid = w4pp_grid(nwg);
+        plan_tail_w4(p, nwg, grid);
         if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(w4pp_grid(nwg)), dim3(256), 0,
-                               s, p);
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(grid), dim3(256), 0, s, p);
         else
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(256), 0, s, p);
+        if (p.tail > 0) {
+            GemmParams q = p;
+            q.tail_only = 1;
+            hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(p.tail * p.split), dim3(NTHREADS), 0, s, q);
+            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
+            count_path(GEMM_PATH_FIXUP);
+        }
     } else if (sc == 10)
         hipLaunchKernelGGL((gemm_bf16_w4p<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
     else if (sc == 2)

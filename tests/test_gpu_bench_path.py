@@ -83,7 +83,8 @@ def test_ln_fold_epilogue_at_bench_shape(N, act, expect):
     finally:
         _lib.lib().ce_set_gemm_schedule(prev)
     cnt = path_counts()
-    assert cnt[expect] == 1 and sum(cnt) == 1, cnt
+    # (plus, on SCHED 11, the split-K tail's fixup when the last round is short)
+    assert cnt[expect] == 1 and sum(cnt) - cnt[FIXUP + FOLD] == 1 and cnt[FIXUP + FOLD] <= 1, cnt
     ref = rstd[:, None] * (A.float() @ Wt.float().t() - mu[:, None] * fold_c[None, :]) + bias
     if act == 1:
         ref = torch.nn.functional.gelu(ref)

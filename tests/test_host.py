@@ -90,26 +90,22 @@ def test_gelu_polynomial_error_bound():
 
 
 def test_gelu_sigmoid_error_bound():
-    """The four-wave GEMM epilogue's GELU (csrc/ce_device.h gelu_fast: x / (1 + 2^(u P(u^2))),
-    u = clamp(x, +-5), degree-4 P) evaluated in f32 as the device does: error <= 1.2e-5 * max(1, |y|)
+    """The four-wave GEMM epilogue's GELU (csrc/ce_device.h gelu_fast4: x / (1 + 2^(u P(u^2))),
+    u = clamp(x, +-X), degree-2 P) evaluated in f32 as the device does: error <= 6.5e-5 * max(1, |y|)
     vs the exact-erf GELU of nn.GELU (transformer.py:235-239) over all x (v_exp_f32 / v_rcp_f32
     modelled as correctly rounded; their 1-ulp error is far inside the bound)."""
     import re
     from scipy.special import erf
     src = open(os.path.join(REPO, "clip-embeds_amd", "csrc", "ce_device.h")).read()
-    body = src[src.index("float gelu_fast"):]
-    body = body[:body.index("return x *")]
-    nums = [np.float32(c) for c in re.findall(r"(-?[0-9]+\.[0-9]+e?-?[0-9]*)f", body)]
-    lim, c4, c3, c2, c1, c0 = nums[1], nums[2], nums[3], nums[4], nums[5], nums[6]
+    k = {n: np.float32(float(v)) for n, v in re.findall(r"#define CE_GELU_(\w+) (-?[0-9.e+-]+)f", src)}
     x = np.linspace(-20, 20, 400001).astype(np.float32)
-    u = np.clip(x, -lim, lim).astype(np.float32)
+    u = np.clip(x, -k["CLAMP"], k["CLAMP"]).astype(np.float32)
     u2 = (u * u).astype(np.float32)
-    p = (u2 * c4 + c3).astype(np.float32)
-    for c in (c2, c1, c0):
-        p = (p * u2 + c).astype(np.float32)
+    p = (u2 * k["C2"] + k["C1"]).astype(np.float32)
+    p = (p * u2 + k["C0"]).astype(np.float32)
     with np.errstate(over="ignore"):
         e = np.exp2((u * p).astype(np.float64)).astype(np.float32)
     r = (1.0 / (np.float32(1) + e).astype(np.float64)).astype(np.float32)
     g = (x * r).astype(np.float32)
     ref = 0.5 * x.astype(np.float64) * (1 + erf(x.astype(np.float64) / np.sqrt(2)))
-    assert (np.abs(g - ref) / np.maximum(1.0, np.abs(ref))).max() <= 1.2e-5
+    assert (np.abs(g - ref) / np.maximum(1.0, np.abs(ref))).max() <= 6.5e-5
