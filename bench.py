@@ -143,9 +143,23 @@ def build_clip(args, dev, rank, world):
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
     scale = float(model.logit_scale.detach().exp())
 
-    def step():
-        fi = model.encode_image(imgs, normalize=True)
-        ft = model.encode_text(caps, normalize=True)
+    # the two towers are independent until the logits: the text tower runs on a second HIP stream
+    # so its kernels fill the image tower's partial last rounds and launch gaps (--serial-towers:
+    # one stream)
+    side = None if args.serial_towers else torch.cuda.Stream(dev)
+
+    def step(concurrent=True):
+        if side is None or not concurrent:
+            fi = model.encode_image(imgs, normalize=True)
+            ft = model.encode_text(caps, normalize=True)
+        else:
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ft = model.encode_text(caps, normalize=True)
+            fi = model.encode_image(imgs, normalize=True)
+            main.wait_stream(side)
+            ft.record_stream(main)
         if world > 1:
             ai = all_gather_cat(fi, world)          # RCCL all-gather over xGMI
             at = all_gather_cat(ft, world)
@@ -282,6 +296,7 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=8, help="pairs per CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    ap.add_argument("--serial-towers", action="store_true", help="clip: both towers on one stream")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -313,7 +328,7 @@ def main():
         # the dominant kernel; inside the timed region only that kernel's launches carry events
         engine.set_timing(True)
         for _ in range(2):
-            step()
+            step(concurrent=False) if args.workload == "clip" else step()
         torch.cuda.synchronize()
         profile = engine.kernel_stats()
         engine.set_timing(False)

@@ -105,6 +105,13 @@ class Engine:
         _lib.call("ce_set_ln_fold", self.h, 1 if on else 0, ctypes.byref(prev))
         return prev.value == 1
 
+    def set_resid_hl(self, on: bool) -> bool:
+        """Keep the folded image tower's residual stream as hi/lo bf16 planes inside the blocks
+        (default on); returns the previous setting (ce_set_resid_hl)."""
+        prev = ctypes.c_int()
+        _lib.call("ce_set_resid_hl", self.h, 1 if on else 0, ctypes.byref(prev))
+        return prev.value == 1
+
     # ---- timing (roofline reporting) ----
     def set_timing(self, on: bool, only: str = ""):
         """Bracket kernel launches with HIP events (all tags, or only the launches tagged `only`)."""

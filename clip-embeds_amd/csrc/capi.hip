@@ -156,6 +156,9 @@ struct ce_handle {
     // LayerNorm folding of the vision blocks: enabled unless CE_LN_FOLD=0 /
     // ce_set_ln_fold(h, 0); folded[name] = "<name>@fold{,_c,_d}" are current for weight `name`
     bool ln_fold = true;
+    // folded image tower: residual stream inside the blocks as hi/lo bf16 planes (EPI_LN_STATS_HL;
+    // env CE_RESID_HL=0 keeps the f32 stream + bf16 copy)
+    bool resid_hl = true;
     std::map<std::string, bool> folded;
     // text-tower training: caller-owned f32 master values and gradient slots per
     // trainable tensor (device pointers), saved activations of the last ce_text_forward_train
@@ -339,6 +342,7 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct TowerWs {
     float* x;
     bf16_t *xn, *qkv, *att, *hid;
+    bf16_t* xlo;          // lo plane right after xn (hi/lo residual stream: plane stride rows * D)
     float* pooled;
     int* rows;
     float* part;     // GEMM split-K partial tiles (ce::kGemmPartElems f32), per tower: the towers may
@@ -350,7 +354,7 @@ struct TowerWs {
 size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
     size_t n = 0;
     n += align256(rows * D * 4);
-    n += align256(rows * D * 2);
+    n += align256(2 * rows * D * 2);
     n += align256(rows * 3 * D * 2);
     n += align256(rows * D * 2);
     n += align256(std::max(rows * F, extra_hid_elems) * 2);
@@ -366,7 +370,9 @@ TowerWs carve(char* base, long rows, int D, int F, long extra_hid_elems, long B)
     TowerWs w;
     char* p = base;
     w.x = (float*)p; p += align256(rows * D * 4);
-    w.xn = (bf16_t*)p; p += align256(rows * D * 2);
+    w.xn = (bf16_t*)p;
+    w.xlo = w.xn + rows * D;
+    p += align256(2 * rows * D * 2);
     w.qkv = (bf16_t*)p; p += align256(rows * 3 * D * 2);
     w.att = (bf16_t*)p; p += align256(rows * D * 2);
     w.hid = (bf16_t*)p; p += align256(std::max(rows * F, extra_hid_elems) * 2);
@@ -426,6 +432,8 @@ struct EpiArgs {
     float2* stats_part = nullptr;
     const float2* fold_stats = nullptr;
     const float* fold_c = nullptr;
+    const bf16_t* rhl = nullptr;     // hi/lo residual planes (EPI_LN_STATS_HL / EPI_HL_F32)
+    long hl_plane = 0;
 };
 
 int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
@@ -441,9 +449,14 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.part = h->cur_part;            // split-K tail slabs of the tower being run (null: no split)
     p.part_elems = h->cur_part ? ce::kGemmPartElems : 0;
     p.xb = ea.xb; p.stats_part = ea.stats_part; p.fold_stats = ea.fold_stats; p.fold_c = ea.fold_c;
+    p.rhl = ea.rhl; p.hl_plane = ea.hl_plane;
     const double flops = 2.0 * M * N * K;
+    // algorithmic bytes: A, W, the residual read (f32 or two bf16 planes: 4 B either way), the output
+    // (f32, bf16, or two bf16 planes) and the bf16 copy of EPI_LN_STATS
+    const bool hl = ea.epi == ce::EPI_LN_STATS_HL || ea.epi == ce::EPI_HL_F32;
     const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
-                         (resid ? (double)M * N * 4 : 0.0) + (ea.xb ? (double)M * N * 2 : 0.0);
+                         ((resid || hl) ? (double)M * N * 4 : 0.0) +
+                         (ea.xb && ea.epi == ce::EPI_LN_STATS ? (double)M * N * 2 : 0.0);
     return timed(h, s, tag, flops, bytes, [&] { return ce::launch_gemm(p, act, out_bf16, s, ea.epi); });
 }
 
@@ -529,6 +542,22 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     st.epi = ce::EPI_LN_STATS;
     st.xb = w.xn;
     st.stats_part = w.stats_part;
+    // hi/lo stream: the residual GEMMs read and rewrite the planes (xn = hi, xlo = lo) in place of
+    // the f32 x and its bf16 copy; the tower's last one writes f32 x for ln_post
+    const bool hl = h->resid_hl;
+    const float* resid = w.x;
+    if (hl) {
+        st.epi = ce::EPI_LN_STATS_HL;
+        st.rhl = w.xn;
+        st.hl_plane = (long)M * D;
+        resid = nullptr;
+    }
+    EpiArgs last_ea;
+    if (hl) {
+        last_ea.epi = ce::EPI_HL_F32;
+        last_ea.rhl = w.xn;
+        last_ea.hl_plane = (long)M * D;
+    }
     auto finalize = [&] {
         return timed(h, s, "ln_stats_v", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
                      [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s); });
@@ -542,16 +571,17 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         CE_TRY(timed(h, s, "attn_v", flops, bytes,
                      [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, false, true, s); }));
     }
-    CE_TRY(gemm(h, s, "gemm_out_v", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, w.x, w.x, false,
+    CE_TRY(gemm(h, s, "gemm_out_v", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, resid, w.x, false,
                 0, 0, 0, 0, 0, st));
     CE_TRY(finalize());
     fold.fold_c = f.cfc;
     CE_TRY(gemm(h, s, "gemm_fc_v", w.xn, D, f.wfc, M, F, D, f.dfc, act_code(h), nullptr, w.hid, true,
                 0, 0, 0, 0, 0, fold));
     if (last) {
-        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, w.x, w.x, false));
+        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
+                    0, 0, 0, 0, 0, last_ea));
     } else {
-        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, w.x, w.x, false,
+        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
                     0, 0, 0, 0, 0, st));
         CE_TRY(finalize());
     }
@@ -582,7 +612,9 @@ int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, b
         p.in = w.x; p.ldi = D; p.out = w.x; p.ldo = D;
         p.w = W(h, "visual.ln_pre.weight"); p.b = W(h, "visual.ln_pre.bias"); p.rows = B * Lv; p.D = D;
         p.xb = w.xn; p.stats = w.stats;
-        CE_TRY(timed(h, s, "ln_v", 0.0, (double)B * Lv * D * 10.0, [&] { return ce::launch_layernorm(p, false, s); }));
+        if (h->resid_hl) p.xlo = w.xlo;
+        CE_TRY(timed(h, s, "ln_v", 0.0, (double)B * Lv * D * (h->resid_hl ? 12.0 : 10.0),
+                     [&] { return ce::launch_layernorm(p, false, s); }));
     } else {
         CE_TRY(layernorm(h, s, "ln_v", w.x, w.x, false, W(h, "visual.ln_pre.weight"), W(h, "visual.ln_pre.bias"),
                          B * Lv, D));
@@ -917,6 +949,7 @@ int ce_create(const ce_config* cfg, int device, ce_handle** out) {
     DeviceGuard g(device);
     ce_handle* h = new ce_handle();
     if (const char* e = getenv("CE_LN_FOLD")) h->ln_fold = atoi(e) != 0;
+    if (const char* e = getenv("CE_RESID_HL")) h->resid_hl = atoi(e) != 0;
     h->cfg = *cfg;
     h->device = device;
     h->G = cfg->image_size / cfg->patch_size;
@@ -1764,7 +1797,8 @@ int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* Wt, int M, 
                             int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
                             void* stats_part, const void* fold_stats, const float* fold_c) {
     if (epi == ce::EPI_PLAIN) return ce_kernel_gemm_bf16(stream, A, Wt, M, N, K, bias, act, resid, out, out_dtype);
-    if (!A || !Wt || !out) return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: null argument");
+    if (!A || !Wt || (!out && epi != ce::EPI_LN_STATS_HL))
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: null argument");
     if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 64)
         return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: need M,N,K > 0, K %% 64 == 0, N %% 64 == 0 (got %d %d %d)",
                     M, N, K);
@@ -1782,6 +1816,17 @@ int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* Wt, int M, 
             return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: LN fold needs no resid, bf16 out, bias, fold_stats, fold_c");
         p.fold_stats = (const float2*)fold_stats;
         p.fold_c = fold_c;
+    } else if (epi == ce::EPI_LN_STATS_HL || epi == ce::EPI_HL_F32) {
+        // residual (and, for 3, output) as hi/lo bf16 planes [2][M][N]
+        if (act != 0 || !resid || (epi == ce::EPI_LN_STATS_HL && (!xb || !stats_part)) ||
+            (epi == ce::EPI_HL_F32 && out_dtype != CE_F32))
+            return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: hi/lo epilogues need act 0, resid planes and "
+                                        "(3) xb planes + stats_part / (4) f32 out");
+        p.resid = nullptr;
+        p.rhl = (const bf16_t*)resid;
+        p.hl_plane = (long)M * N;
+        p.xb = (bf16_t*)xb;
+        p.stats_part = (float2*)stats_part;
     } else {
         return fail(CE_ERR_INVALID, "ce_kernel_gemm_bf16_epi: unknown epilogue %d", epi);
     }
@@ -1815,6 +1860,13 @@ int ce_set_ln_fold(ce_handle* h, int enable, int* previous) {
     if (!h) return fail(CE_ERR_INVALID, "ce_set_ln_fold: null handle");
     if (previous) *previous = h->ln_fold ? 1 : 0;
     h->ln_fold = enable != 0;
+    return CE_OK;
+}
+
+int ce_set_resid_hl(ce_handle* h, int enable, int* previous) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_set_resid_hl: null handle");
+    if (previous) *previous = h->resid_hl ? 1 : 0;
+    h->resid_hl = enable != 0;
     return CE_OK;
 }
 

@@ -27,6 +27,18 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
+// Residual stream as two bf16 planes (EPI_LN_STATS_HL): hi = bf16(v), lo = bf16(v - hi); hi + lo
+// keeps ~16 significand bits (|v - (hi + lo)| <= 2^-17 |v|) in 4 bytes, and hi is exactly the bf16
+// copy the LN-folded GEMMs read as their A operand.
+__device__ __forceinline__ void split_hl(float a, float b, uint32_t& hi, uint32_t& lo) {
+    hi = pack_bf2(a, b);
+    lo = pack_bf2(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+__device__ __forceinline__ float2 join_hl(uint32_t hi, uint32_t lo) {
+    return make_float2(__uint_as_float(hi << 16) + __uint_as_float(lo << 16),
+                       __uint_as_float(hi & 0xffff0000u) + __uint_as_float(lo & 0xffff0000u));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

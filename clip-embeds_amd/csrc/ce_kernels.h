@@ -36,6 +36,11 @@ struct GemmParams {
     float2* stats_part = nullptr;
     const float2* fold_stats = nullptr;
     const float* fold_c = nullptr;
+    // residual stream as two bf16 planes (EPI_LN_STATS_HL / EPI_HL_F32): residual = rhl[m][n] +
+    // rhl[hl_plane + m][n] (row stride ldr); EPI_LN_STATS_HL writes its output the same way into
+    // xb / xb + hl_plane (row stride ldo) instead of out f32 + the bf16 copy
+    const bf16_t* rhl = nullptr;
+    long hl_plane = 0;
     // de-synchronisation of the first round of workgroups (set by launch_gemm): blocks b in
     // [stagger_lo, stagger_hi) with bit `stagger_bit` of b set (stagger_bit < 0: all of them) sleep
     // `stagger` x 127 x 64 cycles before starting, so that later rounds keep half the CUs in their
@@ -45,7 +50,9 @@ struct GemmParams {
     int trace_n = 0;
     int variant = 0;                       // kernel-variant bits for A/B (set_gemm_variant)
 };
-enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2 };
+// EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
+// EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)
+enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2, EPI_LN_STATS_HL = 3, EPI_HL_F32 = 4 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
 // (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
 // combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
@@ -88,6 +95,7 @@ struct LNParams {
     // for an EPI_LN_FOLD consumer
     bf16_t* xb = nullptr;
     float2* stats = nullptr;
+    bf16_t* xlo = nullptr;      // with xb: the lo plane of the hi/lo residual stream (xb = hi)
 };
 hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s);
 

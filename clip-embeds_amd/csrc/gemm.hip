@@ -130,6 +130,10 @@ template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING
 __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f32x4 (&acc)[8][NJ], int mbase,
                                                    int nbase, int lane, const FoldOps<NJ>* pre = nullptr) {
     const int fr = lane & 15, fq = lane >> 4;
+    // LN statistics of the output (x of the residual stream) and the hi/lo bf16 residual planes
+    constexpr bool STATS = EPI == EPI_LN_STATS || EPI == EPI_LN_STATS_HL;
+    constexpr bool HL_IN = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
+    constexpr bool HL_OUT = EPI == EPI_LN_STATS_HL;
     // LN-folded consumer: per-column c_n and per-row (mu, rstd), loaded before any store is issued
     FoldOps<NJ> fo;
     if constexpr (EPI == EPI_LN_FOLD) {
@@ -156,10 +160,27 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
     auto load_resid = [&](int i, float4 (&r)[NJ]) {
         int m = mbase + i * 16 + fr;
         if constexpr (CHECK_M) m = m < p.M ? m : p.M - 1;     // clamp: a valid row, result unused
-        const float* rp = p.resid + (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + nbase + fq * 4;
+        const size_t ro = (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + nbase + fq * 4;
+        if constexpr (HL_IN) {
+            uint2 hi[NJ], lo[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (j < jmax) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
+            for (int j = 0; j < NJ; ++j)
+                if (j < jmax) {
+                    hi[j] = *reinterpret_cast<const uint2*>(p.rhl + ro + j * 16);
+                    lo[j] = *reinterpret_cast<const uint2*>(p.rhl + p.hl_plane + ro + j * 16);
+                }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (j < jmax) {
+                    const float2 a = join_hl(hi[j].x, lo[j].x), c = join_hl(hi[j].y, lo[j].y);
+                    r[j] = make_float4(a.x, a.y, c.x, c.y);
+                }
+        } else {
+            const float* rp = p.resid + ro;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (j < jmax) r[j] = *reinterpret_cast<const float4*>(rp + j * 16);
+        }
     };
     if constexpr (HAS_RESID) {
 #pragma unroll
@@ -167,6 +188,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
     }
     uint2 pend[NJ];      // bf16 output: packed values of the even fragment row, awaiting its partner
     uint2 pxb[NJ];       // EPI_LN_STATS: bf16 copy of the even fragment row (16-B stores as for pend)
+    uint2 plo[NJ];       // EPI_LN_STATS_HL: lo plane of the even fragment row
     // EPI_LN_STATS, per 64-column slab (NJ/4 of them): (mean, M2) of fragment rows fq and fq + 4
     // (this lane stores them) and the running (mean, M2) of this lane's values of the current row
     constexpr int NS = NJ / 4;
@@ -178,7 +200,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
             if (i + RD - 1 < 8) load_resid(i + RD - 1, rbuf[(i + RD - 1) % RD]);
         }
         const int m = mbase + i * 16 + fr;
-        if constexpr (CHECK_M && !OUT_BF16 && EPI != EPI_LN_STATS) {
+        if constexpr (CHECK_M && !OUT_BF16 && !STATS) {
             if (m >= p.M) continue;
         }
         const size_t obase = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + nbase + fq * 4;
@@ -234,10 +256,10 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
             } else {
                 // (the stats epilogue runs the past-the-end rows of the last M tile, with clamped
                 // residual rows, so that each even row still meets its odd partner below)
-                if (EPI != EPI_LN_STATS || !CHECK_M || m < p.M)
+                if (!HL_OUT && (!STATS || !CHECK_M || m < p.M))
                     *reinterpret_cast<float4*>(static_cast<float*>(p.out) + obase + j * 16) =
                         make_float4(v[0], v[1], v[2], v[3]);
-                if constexpr (EPI == EPI_LN_STATS) {
+                if constexpr (STATS) {
                     // Chan's pairwise update: the 4 values of block j join the lane's 4j earlier ones
                     const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
                     const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
@@ -251,9 +273,16 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                         lmean[sl] = fmaf(dl, 1.0f / (jj + 1), lmean[sl]);
                         lm2[sl] += fmaf(dl * dl, 4.0f * jj / (jj + 1), q4);
                     }
-                    const uint2 o = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                    uint2 o, ol;
+                    if constexpr (HL_OUT) {
+                        split_hl(v[0], v[1], o.x, ol.x);
+                        split_hl(v[2], v[3], o.y, ol.y);
+                    } else {
+                        o = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                    }
                     if ((i & 1) == 0) {
                         pxb[j] = o;
+                        if constexpr (HL_OUT) plo[j] = ol;
                     } else {
                         const auto x = __builtin_amdgcn_permlane16_swap(pxb[j].x, o.x, false, false);
                         const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
@@ -261,11 +290,17 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                         const size_t ob = (size_t)mrow * p.ldo + nbase + (fq & ~1) * 4 + j * 16;
                         if ((!CHECK_M || mrow < p.M) && !(p.variant & GEMM_VAR_ABL_NOXB))
                             *reinterpret_cast<uint4*>(p.xb + ob) = make_uint4(x[0], y[0], x[1], y[1]);
+                        if constexpr (HL_OUT) {
+                            const auto xl = __builtin_amdgcn_permlane16_swap(plo[j].x, ol.x, false, false);
+                            const auto yl = __builtin_amdgcn_permlane16_swap(plo[j].y, ol.y, false, false);
+                            if (!CHECK_M || mrow < p.M)
+                                *reinterpret_cast<uint4*>(p.xb + p.hl_plane + ob) = make_uint4(xl[0], yl[0], xl[1], yl[1]);
+                        }
                     }
                 }
             }
         }
-        if constexpr (EPI == EPI_LN_STATS) {
+        if constexpr (STATS) {
             // (mean, M2) of this row's 64-column slab: 4 lanes (fq) of 4*NJ values each, combined
             // with Chan's formula for equal counts
 #pragma unroll
@@ -286,7 +321,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
             }
         }
     }
-    if constexpr (EPI == EPI_LN_STATS) {
+    if constexpr (STATS) {
         // stored after all other stores (no divergent store inside the loop to upset vmcnt counting)
         const int ma = mbase + fq * 16 + fr, mb = ma + 64;
         const size_t ns = p.N / 64;
@@ -1137,18 +1172,37 @@ __global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
         v[0] = apply_act<ACT>(v[0]); v[1] = apply_act<ACT>(v[1]);
         v[2] = apply_act<ACT>(v[2]); v[3] = apply_act<ACT>(v[3]);
     }
+    constexpr bool STATS = EPI == EPI_LN_STATS || EPI == EPI_LN_STATS_HL;
+    constexpr bool HL_IN = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
     if constexpr (HAS_RESID) {
-        const float4 rr = *reinterpret_cast<const float4*>(p.resid + (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + n);
+        const size_t ro = (size_t)map_row(m, p.grp, p.r_gs, p.r_go) * p.ldr + n;
+        float4 rr;
+        if constexpr (HL_IN) {
+            const uint2 hi = *reinterpret_cast<const uint2*>(p.rhl + ro);
+            const uint2 lo = *reinterpret_cast<const uint2*>(p.rhl + p.hl_plane + ro);
+            const float2 a = join_hl(hi.x, lo.x), c = join_hl(hi.y, lo.y);
+            rr = make_float4(a.x, a.y, c.x, c.y);
+        } else {
+            rr = *reinterpret_cast<const float4*>(p.resid + ro);
+        }
         v[0] += rr.x; v[1] += rr.y; v[2] += rr.z; v[3] += rr.w;
     }
     const size_t o = (size_t)map_row(m, p.grp, p.o_gs, p.o_go) * p.ldo + n;
-    if constexpr (OUT_BF16)
+    if constexpr (EPI == EPI_LN_STATS_HL) {
+        uint2 hi, lo;
+        split_hl(v[0], v[1], hi.x, lo.x);
+        split_hl(v[2], v[3], hi.y, lo.y);
+        *reinterpret_cast<uint2*>(p.xb + o) = hi;
+        *reinterpret_cast<uint2*>(p.xb + p.hl_plane + o) = lo;
+    } else if constexpr (OUT_BF16) {
         *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.out) + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-    else
+    } else {
         *reinterpret_cast<float4*>(static_cast<float*>(p.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
-    if constexpr (EPI == EPI_LN_STATS) {
+    }
+    if constexpr (STATS) {
         // a row's 256 columns are one wave (64 threads x 4); a 64-column slab = 16 consecutive lanes
-        *reinterpret_cast<uint2*>(p.xb + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        if constexpr (EPI == EPI_LN_STATS)
+            *reinterpret_cast<uint2*>(p.xb + o) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
         float sm = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
         for (int o2 = 1; o2 < 16; o2 <<= 1) sm += __shfl_xor(sm, o2, 64);
@@ -2027,8 +2081,10 @@ hipError_t launch_w2(const GemmParams& p0, hipStream_t s) {
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
-    if (gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
-    if (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID)) {
+    // the hi/lo residual epilogues exist on SCHED 1 (+ its split-K tail) only
+    constexpr bool HL = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
+    if (!HL && gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
+    if (!HL && (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
         p.gm = gemm_groupm();
         p.stagger = gemm_stagger();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -2055,12 +2111,15 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     p.split = 1;
     plan_tail(p, nwg);
     set_stagger_1(p, nwg);
-    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
-                       dim3(nwg - p.tail + p.tail * p.split), dim3(NTHREADS), 0, s, p);
-    count_path(GEMM_PATH_NT + EPI);
+    constexpr int RG = (EPI == EPI_LN_STATS || EPI == EPI_LN_STATS_HL) ? 3 : CE_RESID_RING;
+    // path counters: the hi/lo epilogues count as their f32-stream counterparts
+    constexpr int CNT = EPI == EPI_LN_STATS_HL ? EPI_LN_STATS : EPI == EPI_HL_F32 ? EPI_PLAIN : EPI;
+    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, RG, EPI>), dim3(nwg - p.tail + p.tail * p.split),
+                       dim3(NTHREADS), 0, s, p);
+    count_path(GEMM_PATH_NT + CNT);
     if (p.tail > 0) {
         hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
-        count_path(GEMM_PATH_FIXUP + EPI);
+        count_path(GEMM_PATH_FIXUP + CNT);
     }
     return hipGetLastError();
 }
@@ -2194,9 +2253,18 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
+    if (p.rhl && epi != EPI_LN_STATS_HL && epi != EPI_HL_F32) return hipErrorInvalidValue;
     if (epi == EPI_LN_STATS) {
         if (act != ACT_NONE || !res || out_bf16 || !p.xb || !p.stats_part) return hipErrorInvalidValue;
         return launch_epi<ACT_NONE, true, false, EPI_LN_STATS>(p, s);
+    }
+    if (epi == EPI_LN_STATS_HL) {
+        if (act != ACT_NONE || !p.rhl || p.hl_plane <= 0 || !p.xb || !p.stats_part || p.grp) return hipErrorInvalidValue;
+        return launch_epi<ACT_NONE, true, false, EPI_LN_STATS_HL>(p, s);
+    }
+    if (epi == EPI_HL_F32) {
+        if (act != ACT_NONE || !p.rhl || p.hl_plane <= 0 || out_bf16 || p.grp) return hipErrorInvalidValue;
+        return launch_epi<ACT_NONE, true, false, EPI_HL_F32>(p, s);
     }
     if (epi == EPI_LN_FOLD) {
         if (res || !out_bf16 || !p.fold_c || !p.fold_stats || !p.bias) return hipErrorInvalidValue;

@@ -100,9 +100,14 @@ __global__ __launch_bounds__(256) void layernorm_k(LNParams p) {
         const float rstd = rsqrtf(wave_sum(q) / (float)D + 1e-5f);
         if (lane == 0) p.stats[orow] = make_float2(mean, rstd);
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
-            *reinterpret_cast<uint2*>(p.xb + (size_t)orow * p.ldo + c * 256 + lane * 4) =
-                make_uint2(pack_bf2(v[c].x, v[c].y), pack_bf2(v[c].z, v[c].w));
+        for (int c = 0; c < NC; ++c) {
+            uint2 hi, lo;
+            split_hl(v[c].x, v[c].y, hi.x, lo.x);
+            split_hl(v[c].z, v[c].w, hi.y, lo.y);
+            const size_t o = (size_t)orow * p.ldo + c * 256 + lane * 4;
+            *reinterpret_cast<uint2*>(p.xb + o) = hi;
+            if (p.xlo) *reinterpret_cast<uint2*>(p.xlo + o) = lo;
+        }
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {

@@ -281,6 +281,10 @@ int ce_gemm_path_counts(int64_t* counts, int n, int reset);
  *   epi 1 (LN stats): out f32 = A W^T + bias + resid; xb = bf16(out); stats_part[m][n/64] = (mean,
  *         sum of squared deviations) of row m's 64-column slab n/64.  act must be 0.
  *   epi 2 (LN fold):  out bf16 = act(fold_stats[m].y * (A W^T - fold_stats[m].x * fold_c[n]) + bias[n]).
+ *   epi 3 (LN stats, hi/lo residual stream): resid = bf16 planes [2][M][N] (value = hi + lo); the
+ *         output v = A W^T + bias + resid goes to xb as planes [2][M][N], hi = bf16(v), lo =
+ *         bf16(v - hi) (out unused); stats_part as epi 1.
+ *   epi 4 (hi/lo residual, f32 out): out f32 = A W^T + bias + (hi + lo) of the resid planes.
  * epi 0 is ce_kernel_gemm_bf16. */
 int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                             int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
@@ -299,6 +303,12 @@ int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int
  * one ce_load_weights call; otherwise the unfolded path runs.  *previous (may be null) gets the
  * previous setting. */
 int ce_set_ln_fold(ce_handle* h, int enable, int* previous);
+/* Residual stream of the LN-folded image tower as two bf16 planes (default on; env CE_RESID_HL=0 at
+ * ce_create): inside the blocks the out-proj / c_proj GEMMs read x = hi + lo and write hi = bf16(x),
+ * lo = bf16(x - hi) (hi doubles as the folded GEMMs' bf16 operand) instead of f32 x plus its bf16
+ * copy: 4 B per element written instead of 6; |x - (hi + lo)| <= 2^-17 |x|.  The tower's last
+ * residual GEMM writes f32 x.  *previous (may be null) gets the previous setting. */
+int ce_set_resid_hl(ce_handle* h, int enable, int* previous);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);
 /* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */

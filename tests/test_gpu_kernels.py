@@ -194,6 +194,44 @@ def test_gemm_persistent_ln_stats(M, K, bits):
     assert bool((out[M:] == 7.0).all()) and bool((xb[M:] == 7.0).all()) and bool((part[M:] == 7.0).all())
 
 
+@pytest.mark.parametrize("M,K", [(147712, 1024), (147712, 4096), (300, 1024), (5000, 1024)])
+def test_gemm_ln_stats_hl(M, K):
+    """The hi/lo residual-stream epilogues (SCHED 1, split-K tail at the bench shapes M = 256 * 577):
+    epi 3 reads resid = hi + lo and writes v = A W^T + b + resid as planes hi = bf16(v),
+    lo = bf16(v - hi) plus the slab statistics; epi 4 writes v in f32.  vs torch f32: hi is the
+    round-to-nearest bf16 of v, hi + lo within 2^-16 |v| of v (f32 accumulation order aside)."""
+    N = 1024
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    x = torch.randn(M, N, generator=g).to(DEV)
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    planes = torch.stack([hi, lo]).contiguous()
+    ref = A.float() @ W.float().t() + bias + (hi.float() + lo.float())
+    ns = N // 64
+    outp = torch.full((2, M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    part = torch.full((M, ns, 2), 7.0, device=DEV)
+    _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), None, _lib.CE_F32,
+              3, P(outp), P(part), None, None)
+    out4 = torch.empty(M, N, device=DEV)
+    _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), P(out4), _lib.CE_F32,
+              4, None, None, None, None)
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (out4 - ref).abs().max().item() <= 2e-4 * scale + 1e-5
+    v = outp[0].float() + outp[1].float()
+    assert (v - ref).abs().max().item() <= 2e-4 * scale + 1e-5
+    assert (v - out4).abs().max().item() <= 2 ** -16 * scale
+    assert torch.equal(outp[0], v.to(torch.bfloat16)) or (outp[0].float() - v).abs().max().item() <= 2 ** -8 * scale
+    r3 = ref.reshape(M, ns, 64)
+    mean = r3.mean(-1)
+    m2 = ((r3 - mean[..., None]) ** 2).sum(-1)
+    assert (part[:, :, 0] - mean).abs().max().item() <= 1e-4 * scale
+    assert (part[:, :, 1] - m2).abs().max().item() <= 1e-4 * m2.abs().max().item() + 1e-4
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric W catches a transposed C-write (guide §3)."""
     n = 256

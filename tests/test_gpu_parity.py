@@ -148,6 +148,30 @@ def _ran_folded(m, fn):
     return out, "ln_stats_v" in names
 
 
+def test_resid_hl_matches_f32_stream():
+    """The folded image tower with its residual stream as hi/lo bf16 planes (default) vs the f32
+    stream + bf16 copy, full depth: pooled and token outputs within 1e-5 cosine of each other
+    (|x - (hi + lo)| <= 2^-17 |x| per residual GEMM) and within 1e-3 of the golden."""
+    cfg = get_model_config("ViT-L-14-336")
+    m = make_model(cfg)
+    imgs = torch.from_numpy(W.synthetic_images(3, seed=98))
+    m.visual.output_tokens = True
+    try:
+        ph, th = m.encode_image(imgs)
+        prev = m._engine.set_resid_hl(False)
+        assert prev
+        try:
+            pf, tf = m.encode_image(imgs)
+        finally:
+            m._engine.set_resid_hl(True)
+        assert cos_dist(ph.cpu().numpy(), pf.cpu().numpy()) < 1e-5
+        assert cos_dist(th.cpu().numpy()[:, ROWS_V], tf.cpu().numpy()[:, ROWS_V]) < 1e-5
+        o = O.encode_image(W.synthetic_state_dict(cfg), imgs.numpy(), cfg)
+        assert cos_dist(ph.cpu().numpy(), o) < COS_TOL
+    finally:
+        m.visual.output_tokens = False
+
+
 def test_ln_fold_matches_unfolded():
     """Image tower with ln_1/ln_2 folded into in_proj/c_fc (default) vs the LayerNorm path, at full
     depth: pooled and token outputs within 2e-4 cosine of each other and both within 1e-3 of the
