@@ -147,6 +147,9 @@ def build_clip(args, dev, rank, world):
     # so its kernels fill the image tower's partial last rounds and launch gaps (--serial-towers:
     # one stream)
     side = None if args.serial_towers else torch.cuda.Stream(dev)
+    # --tower-priority: the image tower (the critical path) on a high-priority stream, so the
+    # dispatcher prefers its workgroups and the text tower only fills gaps
+    hp = torch.cuda.Stream(dev, priority=-1) if (side is not None and args.tower_priority) else None
 
     def step(concurrent=True):
         if side is None or not concurrent:
@@ -157,7 +160,14 @@ def build_clip(args, dev, rank, world):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 ft = model.encode_text(caps, normalize=True)
-            fi = model.encode_image(imgs, normalize=True)
+            if hp is None:
+                fi = model.encode_image(imgs, normalize=True)
+            else:
+                hp.wait_stream(main)
+                with torch.cuda.stream(hp):
+                    fi = model.encode_image(imgs, normalize=True)
+                main.wait_stream(hp)
+                fi.record_stream(main)
             main.wait_stream(side)
             ft.record_stream(main)
         if world > 1:
@@ -297,6 +307,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--serial-towers", action="store_true", help="clip: both towers on one stream")
+    ap.add_argument("--tower-priority", action="store_true", help="clip: image tower on a high-priority stream")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

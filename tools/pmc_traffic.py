@@ -14,6 +14,9 @@ import os
 import sys
 
 KERNEL = {"attn_v": "attn_fwd", "attn_t": "attn_fwd", "ln_v": "layernorm_k"}
+# tools/pmc_traffic2.sh shapes (bench_gemm_epi names): the main GEMM kernel of the launch (the
+# persistent four-wave kernel for qkv / fc, the 4-phase kernel for out / proj)
+KERNEL2 = {"qkv": "gemm_bf16_w4pp", "fc": "gemm_bf16_w4pp", "out": "gemm_bf16_nt", "proj": "gemm_bf16_nt"}
 
 
 def avg_counter(d, counter, kname):
@@ -31,12 +34,12 @@ def main():
     res = {}
     shapes = sorted({os.path.basename(p).rsplit("_", 2)[0] for p in glob.glob(os.path.join(root, "*_FETCH_SIZE"))})
     for s in shapes:
-        kname = KERNEL.get(s, "gemm_bf16_nt")
+        kname = KERNEL.get(s, KERNEL2.get(s, "gemm_bf16_nt"))
         fetch, nf = avg_counter(os.path.join(root, f"{s}_FETCH_SIZE"), "FETCH_SIZE", kname)
         write, nw = avg_counter(os.path.join(root, f"{s}_WRITE_SIZE"), "WRITE_SIZE", kname)
         if fetch is None or write is None:
             continue
-        tag = s if s in KERNEL else "gemm_" + s
+        tag = s if s in KERNEL else "gemm_" + (s + "_v" if s in KERNEL2 else s)
         res[tag] = {"hbm_bytes_per_launch": round((2 * fetch + write) * 1024),
                     "fetch_bytes_corrected": round(2 * fetch * 1024), "write_bytes": round(write * 1024),
                     "dispatches": [nf, nw], "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {root}"}
