@@ -121,9 +121,11 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        // split-K tail on the four-wave persistent schedule (a last round of <= 1/8 of the grid)
        GEMM_VAR_W4_TAIL = 32,
        // timing ablation of the LN-statistics epilogues: no bf16 copy of the output (wrong xb)
-       GEMM_VAR_ABL_NOXB = 64 };
+       GEMM_VAR_ABL_NOXB = 64,
+       // the hi/lo residual GEMMs (EPI_LN_STATS_HL) on the staged-residual four-wave kernel
+       GEMM_VAR_W4_RHL = 128 };
 #ifndef CE_GEMM_VAR_DEFAULT
-#define CE_GEMM_VAR_DEFAULT (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2)
+#define CE_GEMM_VAR_DEFAULT (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL)
 #endif
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
@@ -362,6 +364,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x4 (
 //    addresses are one 32-bit VGPR (row-pair step added to it, 16-column step in the immediate);
 //  * two fragment rows are paired with v_permlane16_swap so each lane stores 16 B (8 columns).
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
 
 template <int ACT>
 __device__ __forceinline__ float w4_act(float v) {
@@ -1719,6 +1722,371 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// The lane id recomputed where it is used (volatile: never hoisted out of a loop or merged with
+// another copy, so lane-derived offsets are rematerialised instead of held in spilled VGPRs)
+__device__ __forceinline__ int fresh_lane_id() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// Sum over the four 16-lane groups of a wave (lanes l, l^16, l^32, l^48) with two lane-swap pairs
+// (no LDS permute, no lane-id arithmetic)
+__device__ __forceinline__ float sum_lane_groups(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// ------------------------------------------------------------------------------------------
+// SCHED 11 for the residual GEMMs of the folded image tower (out-proj / c_proj with
+// EPI_LN_STATS_HL: x += A W^T + b on the hi/lo bf16 planes, LN slab statistics).  SCHED 11's
+// epilogue pays vmcnt's issue order twice: a residual load waits for every store issued before it,
+// and the next tile's DMAs (issued before the epilogue) sit behind nothing, but the ones after it sit
+// behind all its stores.  This variant orders the traffic so that no wait covers a store that has not
+// had half an epilogue or a K-tile to drain:
+//  * the last two K-tiles of a tile DMA the residual of fragment rows 0-3 of every wave (hi plane at
+//    K-tile nk-2, lo plane at nk-1, each into the stage buffer that K-tile frees, 64 KB per plane,
+//    16-B chunks XOR-swizzled by row) in place of the next tile's first K-tiles;
+//  * the epilogue (a) loads the residual of fragment rows 4-5 into registers (before any store),
+//    (b) finishes rows 0-3 from LDS and stores them, (a2) loads rows 6-7, (c) releases the LDS,
+//    (d) issues the next tile's bias and K-tiles 0 and 1, (e) finishes rows 4-7 from registers and
+//    stores them plus the slab statistics;
+//  * the next tile waits for its K-tile 0 with vmcnt(52): the 36 stores of (e) and the 16 DMAs of
+//    K-tile 1 may stay in flight.
+// Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.
+__global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char* const side = smem + 2 * STAGE_BYTES + wave * W4_SIDE_BYTES;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_n = p.N / BN;
+    const int nwg = tiles_m * tiles_n;
+    const int grid = gridDim.x;
+    const int slot = xcd_remap(blockIdx.x, grid);
+    const int nk = p.K / BK;
+    const int my_tiles = slot < nwg ? (nwg - 1 - slot) / grid + 1 : 0;
+    // de-synchronised start (p.stagger x s_sleep 127 for the odd slots): equal tiles keep the CUs in
+    // lock-step, K-loops (MFMA-bound) and epilogues (HBM-bound) each chip-wide at once
+    if (p.stagger > 0 && (slot & 1))
+        for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+
+    // per-lane DMA source offsets of a K-tile (A rows, W rows; 16-B chunks swizzled by row pair)
+    auto k_offsets = [&](int ln, int& vA, int& vW) {
+        const int srow = wave * 8 + (ln >> 3);
+        const int schunk = (ln & 7) ^ ((srow >> 1) & 7);
+        vA = srow * (int)p.lda * 2 + schunk * 16;
+        vW = srow * (int)p.ldw * 2 + schunk * 16;
+    };
+    int voffA, voffW;
+    k_offsets(lane, voffA, voffW);
+    const int jstrA = 32 * (int)p.lda * 2, jstrW = 32 * (int)p.ldw * 2;
+    __amdgpu_buffer_rsrc_t srdA, srdW, srdH, srdL;
+    int m0 = 0, n0 = 0;
+    auto set_tile = [&](int t) {
+        int tm, tn;
+        tile_of(slot + t * grid, tiles_m, tiles_n, p.gm, tm, tn);
+        m0 = tm * BM;
+        n0 = tn * BN;
+        const int rows = max(0, min(p.M - m0, BM));
+        srdA = make_srd(p.A + (size_t)m0 * p.lda, rows * (int)p.lda * 2);
+        srdW = make_srd(p.W + (size_t)n0 * p.ldw, BN * (int)p.ldw * 2);
+        srdH = make_srd(p.rhl + (size_t)m0 * p.ldr, rows * (int)p.ldr * 2);
+        srdL = make_srd(p.rhl + p.hl_plane + (size_t)m0 * p.ldr, rows * (int)p.ldr * 2);
+    };
+    // K-tile kt of the current tile into stage buffer `buf` (16 DMAs per thread)
+    // (scalar operands are derived from opaque copies so that the 16 per-instruction offsets and LDS
+    // addresses are recomputed at each issue instead of being hoisted into spilled SGPRs)
+    auto dma_k = [&](int buf, int kt, int j, int voffA, int voffW) {
+        int lb = buf * STAGE_BYTES + wave * 8 * 128;
+        int st = j < 8 ? jstrA : jstrW;
+        asm volatile("" : "+s"(lb), "+s"(st));
+        char* base = smem + lb;
+        const int jo = (j < 8 ? j : j - 8) * st;
+        if (j < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + j * 32 * 128), 16, voffA + jo, kt * BK * 2, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + TILE_BYTES + (j - 8) * 32 * 128), 16,
+                                                     voffW + jo, kt * BK * 2, 0, 0);
+    };
+    // residual plane (0 hi, 1 lo) of the staged rows into stage buffer `plane`: staged row
+    // r = 0..127 is tile row (r >> 6) * 128 + (r & 63) (fragment rows 0-3 of the two wave rows),
+    // 512 B (256 columns), 16-B chunk c of row r at c ^ (r & 15)
+    // (the row offset stays in voffset, where the descriptor clips it at row M; the column offset
+    // n0 goes to soffset; per-instruction row offsets are opaque so they are not hoisted to VGPRs)
+    const int rpair = wave * 2 + (lane >> 5);                   // r & 7 of the staged row
+    const int vr0 = (lane >> 5) * (int)p.ldr * 2 + ((lane & 31) ^ rpair) * 16;
+    const int vr1 = (lane >> 5) * (int)p.ldr * 2 + ((lane & 31) ^ (rpair | 8)) * 16;
+    auto dma_r = [&](int buf, int plane, int j) {
+        int lb = buf * STAGE_BYTES + wave * 2 * 512;
+        int l2 = (int)p.ldr * 2;
+        asm volatile("" : "+s"(lb), "+s"(l2));
+        const int ro = (j * 8 + wave * 2 + (j >= 8 ? 64 : 0)) * l2;
+        char* base = smem + lb + j * 8 * 512;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(plane ? srdL : srdH, (CE_LDS void*)base, 16, ((j & 1) ? vr1 : vr0) + ro,
+                                                 n0 * 2, 0, 0);
+    };
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const int fo0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
+    const int fo1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
+    const int a_off = wm * 128 * 128;
+    const int w_off = TILE_BYTES + wn * 128 * 128;
+
+    f32x4 acc[8][8];
+    bf16x8 a0[8], b0[8], a1[8], b1[8];
+#define CE_MFMA_AGPR(ACC, BV, AV) \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
+    auto read_set0 = [&](const char* sb0) __attribute__((always_inline)) {
+        int bo = 0;
+        asm volatile("" : "+s"(bo));
+        const char* sb = sb0 + bo;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            b0[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo0);
+            a0[q] = *reinterpret_cast<const bf16x8*>(sb + a_off + q * 16 * 128 + fo0);
+        }
+    };
+    // one K-tile: B1 | barrier | B2 + 16 DMAs | wait + barrier | B3 (as SCHED 11).  MODE 0: the
+    // DMAs fetch K-tile kt + 2 and B3 prefetches set 0 of K-tile kt + 1; MODE 1 (kt = nk - 2): they
+    // fetch the hi residual plane; MODE 2 (kt = nk - 1): the lo plane, no prefetch
+    auto ktile = [&](int kt, int wait_n, auto mode) __attribute__((always_inline)) {
+        constexpr int MODE = decltype(mode)::value;
+        const int buf = kt & 1;
+        // stage-buffer bases from an opaque scalar: the fragment addresses are formed per K-tile
+        // instead of being kept (and spilled) for both buffers
+        int bo = buf * STAGE_BYTES;
+        asm volatile("" : "+s"(bo));
+        const char* sb = smem + bo;
+        const char* so = smem + (STAGE_BYTES - bo);
+#pragma unroll
+        for (int s2 = 0; s2 < 32; ++s2) {
+            const int i = s2 >> 3, j = s2 & 7;
+            CE_MFMA_AGPR(acc[i][j], b0[j], a0[i]);
+            if (s2 & 1) {
+                const int q = s2 >> 1;
+                if (q < 8) b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
+                else a1[q - 8] = *reinterpret_cast<const bf16x8*>(sb + a_off + (q - 8) * 16 * 128 + fo1);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+        // K-tile kt + 2, or for the last two K-tiles the residual planes, into this buffer
+#pragma unroll
+        for (int s2 = 0; s2 < 64; ++s2) {
+            const int i = (s2 >> 3) & 3, j = s2 & 7;
+            if (s2 < 32) CE_MFMA_AGPR(acc[4 + i][j], b0[j], a0[4 + i]);
+            else CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
+            if ((s2 & 3) == 3) {
+                if constexpr (MODE == 0) dma_k(buf, kt + 2, s2 >> 2, voffA, voffW);
+                else dma_r(buf, MODE - 1, s2 >> 2);
+            }
+        }
+        if (wait_n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else if (wait_n == 52) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+#pragma unroll
+        for (int s2 = 0; s2 < 32; ++s2) {
+            const int i = s2 >> 3, j = s2 & 7;
+            CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+            if constexpr (MODE < 2) {
+                if (s2 & 1) {
+                    const int q = s2 >> 1;
+                    if (q == 0) a0[0] = *reinterpret_cast<const bf16x8*>(so + a_off + fo0);
+                    else if (q < 9) b0[q - 1] = *reinterpret_cast<const bf16x8*>(so + w_off + (q - 1) * 16 * 128 + fo0);
+                    else a0[q - 8] = *reinterpret_cast<const bf16x8*>(so + a_off + (q - 8) * 16 * 128 + fo0);
+                }
+            }
+        }
+    };
+    using K_ = std::integral_constant<int, 0>;
+    using R0_ = std::integral_constant<int, 1>;
+    using R1_ = std::integral_constant<int, 2>;
+
+    const int ldo = (int)p.ldo, ldr = (int)p.ldr;
+    constexpr int NS = 2;                                       // 64-column slabs per wave quadrant
+    if (my_tiles > 0) {
+        set_tile(0);
+        w4_side_fill<EPI_PLAIN>(p, side, m0 + wm * 128, n0 + wn * 128, lane);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dma_k(0, 0, j, voffA, voffW);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dma_k(1, 1, j, voffA, voffW);
+    }
+    for (int t = 0; t < my_tiles; ++t) {
+        // K-tile 0 landed: the younger ops are K-tile 1's 16 DMAs and (t > 0) the 32 stores of the
+        // previous epilogue's rows 4-7 + its 4 slab-statistics stores, which keep draining
+        if (t == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
+        barrier();
+        {
+            // the accumulators start at the bias (DMA'd to the side area ahead of K-tile 0)
+            // (read with asm ds_reads: the bias DMA is older than K-tile 0, which the wait above
+            // retired, but the compiler would wait for every LDS-DMA in flight, K-tile 1's included)
+            const int lnb = fresh_lane_id();
+            const unsigned ba = (unsigned)(uintptr_t)(CE_LDS void*)side + (lnb >> 4) * 16;
+            f32x4 bv[8];
+#define CE_RD(J) asm volatile("ds_read_b128 %0, %1 offset:" #J "" : "=v"(bv[J / 64]) : "v"(ba))
+            CE_RD(0); CE_RD(64); CE_RD(128); CE_RD(192); CE_RD(256); CE_RD(320); CE_RD(384); CE_RD(448);
+#undef CE_RD
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j] = bv[j];
+        }
+        read_set0(smem);
+        trace_stamp(p, 0, t * grid + blockIdx.x);
+        // K-tile kt + 1 landed (kt = 0 of a later tile: the previous epilogue's 36 stores are younger
+        // than K-tile 1 too)
+        for (int kt = 0; kt < nk - 2; ++kt) ktile(kt, (kt == 0 && t > 0) ? 52 : 16, K_{});
+        ktile(nk - 2, (nk == 2 && t > 0) ? 52 : 16, R0_{});
+        ktile(nk - 1, 0, R1_{});                // residual planes landed for every wave
+        trace_stamp(p, 1, t * grid + blockIdx.x);
+
+        const int mbase = m0 + wm * 128, nbase = n0 + wn * 128;
+        // lane-derived offsets from an opaque copy of the lane id: recomputed per tile rather than
+        // hoisted out of the tile loop into (spilled) registers
+        const int lne = fresh_lane_id();
+        const int fre = lne & 15, fqe = lne >> 4;
+        const int rows = max(0, min(p.M - mbase, 128));
+        // (a) residual of fragment rows 4-5 into registers before any store (per-row offsets are
+        // opaque: hoisted, they would be spilled, and a scratch reload waits for every store)
+        const __amdgpu_buffer_rsrc_t hs = make_srd(p.rhl + (size_t)mbase * ldr, rows * ldr * 2);
+        const __amdgpu_buffer_rsrc_t ls = make_srd(p.rhl + p.hl_plane + (size_t)mbase * ldr, rows * ldr * 2);
+        const int ro = (fre * ldr + nbase + fqe * 4) * 2;
+        auto load_rows = [&](uint2 (&h)[2][8], uint2 (&l)[2][8], int i0) __attribute__((always_inline)) {
+            int io = i0 * 16 * ldr * 2, st = 16 * ldr * 2;
+            asm volatile("" : "+s"(io), "+s"(st));
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int vo = ro + io + i * st;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    h[i][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(hs, vo + j * 32, 0, 0));
+                    l[i][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ls, vo + j * 32, 0, 0));
+                }
+            }
+        };
+        uint2 rah[2][8], ral[2][8], rbh[2][8], rbl[2][8];
+        load_rows(rah, ral, 4);
+        const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
+        const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
+        int xo = ((fre + (fqe & 1) * 16) * ldo + nbase + (fqe >> 1) * 8) * 2;
+        float2 sta[NS], stb[NS];                 // initialised: not carried across tiles
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) sta[sl] = stb[sl] = make_float2(0.f, 0.f);
+        // fragment rows i0 and i0 + 1: v = acc (+ bias) + residual; (mean, M2) per 64-column slab;
+        // hi/lo planes of the two rows paired by v_permlane16_swap into 16-B stores
+        auto row_pair = [&](int i0, auto get_r) __attribute__((always_inline)) {
+            float lmean[2][NS], lm2[2][NS];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint2 h[2], l[2];
+#pragma unroll
+                for (int r2 = 0; r2 < 2; ++r2) {
+                    f32x4 v = acc[i0 + r2][j];
+                    const float4 r = get_r(i0 + r2, j);
+                    v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+                    const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+                    const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
+                    const float q4 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
+                    const int sl = j >> 2, jj = j & 3;
+                    if (jj == 0) {
+                        lmean[r2][sl] = m4;
+                        lm2[r2][sl] = q4;
+                    } else {
+                        const float dl = m4 - lmean[r2][sl];
+                        lmean[r2][sl] = fmaf(dl, 1.0f / (jj + 1), lmean[r2][sl]);
+                        lm2[r2][sl] += fmaf(dl * dl, 4.0f * jj / (jj + 1), q4);
+                    }
+                    split_hl(v[0], v[1], h[r2].x, l[r2].x);
+                    split_hl(v[2], v[3], h[r2].y, l[r2].y);
+                }
+                const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
+                const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
+                const auto xx = __builtin_amdgcn_permlane16_swap(l[0].x, l[1].x, false, false);
+                const auto yy = __builtin_amdgcn_permlane16_swap(l[0].y, l[1].y, false, false);
+                const u32x4 dh = {x[0], y[0], x[1], y[1]};
+                const u32x4 dl = {xx[0], yy[0], xx[1], yy[1]};
+                __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
+            }
+            xo += 32 * ldo * 2;
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const int i = i0 + r2;
+#pragma unroll
+                for (int sl = 0; sl < NS; ++sl) {
+                    const float mean = sum_lane_groups(lmean[r2][sl]) * 0.25f;
+                    const float dl = lmean[r2][sl] - mean;
+                    const float q = sum_lane_groups(fmaf(dl * dl, 16.0f, lm2[r2][sl]));
+                    if (fqe == (i & 3)) {
+                        if (i < 4) sta[sl] = make_float2(mean, q);
+                        else stb[sl] = make_float2(mean, q);
+                    }
+                }
+            }
+        };
+        // (b) fragment rows 0-3: residual from the staged planes
+        const int lr0 = ((nk - 2) & 1) * STAGE_BYTES + (wm * 64 + fre) * 512;
+        const int llo = (((nk - 1) & 1) - ((nk - 2) & 1)) * STAGE_BYTES;
+        auto lds_r = [&](int i, int j) {
+            const int c = (wn * 16 + 2 * j + (fqe >> 1)) ^ fre;        // staged row r has r & 15 == fre
+            const int off = lr0 + i * 16 * 512 + (c << 4) + (fqe & 1) * 8;
+            const uint2 h = *reinterpret_cast<const uint2*>(smem + off);
+            const uint2 l = *reinterpret_cast<const uint2*>(smem + llo + off);
+            const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
+            return make_float4(a.x, a.y, b.x, b.y);
+        };
+        row_pair(0, lds_r);
+        asm volatile("" ::: "memory");          // rows 2-3's LDS reads stay behind rows 0-1 (VGPRs)
+        row_pair(2, lds_r);
+        // (a2) residual of rows 6-7 (behind the 32 stores of (b), ahead of the next tile's DMAs)
+        load_rows(rbh, rbl, 6);
+        // (c) every wave's LDS residual reads done -> (d) the next tile's bias and K-tiles 0 and 1
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+        if (t + 1 < my_tiles) {
+            set_tile(t + 1);
+            w4_side_fill<EPI_PLAIN>(p, side, m0 + wm * 128, n0 + wn * 128, lne);
+            int vA, vW;
+            k_offsets(lne, vA, vW);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dma_k(0, 0, j, vA, vW);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dma_k(1, 1, j, vA, vW);
+        }
+        // (e) fragment rows 4-7 from the registers of (a) and (a2)
+        auto reg_r = [&](int i, int j) {
+            const uint2 h = i < 6 ? rah[i - 4][j] : rbh[i - 6][j], l = i < 6 ? ral[i - 4][j] : rbl[i - 6][j];
+            const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
+            return make_float4(a.x, a.y, b.x, b.y);
+        };
+        row_pair(4, reg_r);
+        row_pair(6, reg_r);
+        // slab statistics: rows fqe and fqe + 4 of this lane's 16-row groups (clipped at M)
+        {
+            const int ns = p.N / 64;
+            const __amdgpu_buffer_rsrc_t ss = make_srd(p.stats_part + (size_t)mbase * ns, rows * ns * 8);
+            const int so = ((fqe * 16 + fre) * ns + nbase / 64) * 8;
+#pragma unroll
+            for (int sl = 0; sl < NS; ++sl) {
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, sta[sl]), ss, so + sl * 8, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, stb[sl]), ss, so + 64 * ns * 8 + sl * 8, 0, 0);
+            }
+        }
+        trace_stamp(p, 2, t * grid + blockIdx.x);
+    }
+#undef CE_MFMA_AGPR
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------------------------------------------------
 // SCHED 12 ("w2"): TWO 256-thread workgroups per CU, each computing a 256 x 128 tile with four
 // waves of 128 x 64 (2 x 2; acc[8][4] of v_mfma_f32_16x16x32_bf16, the SCHED 1 per-wave tile and
@@ -2083,6 +2451,20 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
     // the hi/lo residual epilogues exist on SCHED 1 (+ its split-K tail) only
     constexpr bool HL = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
+    if constexpr (EPI == EPI_LN_STATS_HL) {
+        // staged-residual four-wave kernel (default policy): whole 256-column tiles, >= 2 K-tiles,
+        // a grid of >= 2 tiles per CU (no split-K tail); CE_GEMM_AUTO=0 or a pinned schedule keeps
+        // SCHED 1 (r02 A/B at B = 256: out-proj 682 vs 589 TF/s, c_proj 1,092 vs 995)
+        const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
+        if ((gemm_variant() & GEMM_VAR_W4_RHL) && gemm_auto() != 0 && gemm_sched() == 1 && p.N % BN == 0 &&
+            p.K >= 2 * BK && nwg >= 2 * num_cus()) {
+            p.gm = gemm_groupm();
+            p.stagger = gemm_stagger();
+            hipLaunchKernelGGL(gemm_w4_resid_hl, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            count_path(GEMM_PATH_W4PP + EPI_LN_STATS);
+            return hipGetLastError();
+        }
+    }
     if (!HL && gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     if (!HL && (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
         p.gm = gemm_groupm();

@@ -265,11 +265,14 @@ int ce_set_gemm_splitk(int enable);
  * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
 int ce_set_gemm_auto(int mode);
 /* GEMM kernel-variant bits for A/B measurement (env CE_GEMM_VARIANT at first use; a negative value
- * restores the default, bits 0|1): bit 0 = the four-wave persistent schedule does not drain an
+ * restores the default, bits 0|1|7): bit 0 = the four-wave persistent schedule does not drain an
  * epilogue's stores at the next tile's first K-tile; bit 1 = its epilogue written for one wave per
  * SIMD (operands staged in LDS, clipped buffer stores; also lets the default policy put GELU GEMMs on
- * that schedule); bits 2, 3 = timing ablations of its LN-statistics epilogue (no residual loads /
- * no stores: wrong outputs).  Returns the previous bits. */
+ * that schedule); bits 2, 3, 6 = timing ablations of the LN-statistics epilogues (no residual loads /
+ * no stores / no bf16 copy: wrong outputs); bit 4 = one tile per four-wave workgroup; bit 5 = split-K
+ * tail on the four-wave schedule; bit 7 = the hi/lo residual GEMMs (epi 3, N % 256 == 0, grids of
+ * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel.
+ * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other

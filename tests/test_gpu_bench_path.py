@@ -173,11 +173,12 @@ def test_batch256_full_depth_bench_path(full_model, golden):
         pi, ti = m.encode_image(imgs)
         torch.cuda.synchronize()
         cnt = path_counts()
-        # 24 QKV + 24 c_fc on SCHED 11 + LN fold; 24 out-proj + 23 c_proj with LN stats, each with
-        # a split-K tail (the last c_proj is plain: nothing consumes its stats)
+        # 24 QKV + 24 c_fc on SCHED 11 + LN fold; 24 out-proj + 23 c_proj with LN stats on the hi/lo
+        # stream on the staged-residual four-wave kernel (the last c_proj writes the f32 stream:
+        # nothing consumes its stats)
         assert cnt[W4PP + FOLD] == 48, cnt
         assert cnt[NT + FOLD] == 0, cnt
-        assert cnt[NT + STATS] == 47 and cnt[FIXUP + STATS] == 47, cnt
+        assert cnt[W4PP + STATS] == 47 and cnt[NT + STATS] == 0 and cnt[FIXUP + STATS] == 0, cnt
         pt = m.encode_text(caps)
         pi_n, ti_n, pt_n = pi.cpu().numpy(), ti.cpu().numpy(), pt.cpu().numpy()
         sel = [0, 255]
@@ -234,7 +235,7 @@ def test_pacl_batch512_golden_rows(golden, tag):
     a, b = mod(torch.from_numpy(imgs).to(DEV), torch.from_numpy(caps).to(DEV))
     torch.cuda.synchronize()
     cnt = path_counts()
-    assert cnt[W4PP + FOLD] == 4 and cnt[FIXUP + STATS] >= 1, cnt       # the big-grid paths ran
+    assert cnt[W4PP + FOLD] == 4 and cnt[W4PP + STATS] >= 1, cnt       # the big-grid paths ran
     a, b = a.cpu().numpy(), b.cpu().numpy()
     assert cos_dist(a[[0, 511]], g[f"{tag}_img"]) < COS_TOL
     assert cos_dist(b[[0, 511]], g[f"{tag}_txt"]) < COS_TOL

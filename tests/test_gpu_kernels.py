@@ -20,6 +20,13 @@ def S():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def path_counts():
+    """ce_gemm_path_counts, reset after reading (indices: include/clipembed.h)."""
+    c = (ctypes.c_int64 * 13)()
+    _lib.call("ce_gemm_path_counts", c, 13, 1)
+    return list(c)
+
+
 def gemm_ref(A, W, bias, act, resid):
     y = A.float() @ W.float().t()
     if bias is not None:
@@ -194,13 +201,17 @@ def test_gemm_persistent_ln_stats(M, K, bits):
     assert bool((out[M:] == 7.0).all()) and bool((xb[M:] == 7.0).all()) and bool((part[M:] == 7.0).all())
 
 
-@pytest.mark.parametrize("M,K", [(147712, 1024), (147712, 4096), (300, 1024), (5000, 1024)])
-def test_gemm_ln_stats_hl(M, K):
-    """The hi/lo residual-stream epilogues (SCHED 1, split-K tail at the bench shapes M = 256 * 577):
-    epi 3 reads resid = hi + lo and writes v = A W^T + b + resid as planes hi = bf16(v),
-    lo = bf16(v - hi) plus the slab statistics; epi 4 writes v in f32.  vs torch f32: hi is the
-    round-to-nearest bf16 of v, hi + lo within 2^-16 |v| of v (f32 accumulation order aside)."""
-    N = 1024
+@pytest.mark.parametrize("M,K,N,rhl", [(147712, 1024, 1024, 0), (147712, 4096, 1024, 0), (300, 1024, 1024, 0),
+                                       (5000, 1024, 1024, 0), (147712, 1024, 1024, 1), (147712, 4096, 1024, 1),
+                                       (140001, 1024, 1024, 1), (131072, 192, 768, 1), (70000, 128, 1536, 1)])
+def test_gemm_ln_stats_hl(M, K, N, rhl):
+    """The hi/lo residual-stream epilogues (SCHED 1, split-K tail at the bench shapes M = 256 * 577;
+    rhl: epi 3 on the staged-residual four-wave kernel, variant bit 128, incl. a ragged last row
+    tile, K = 2 and 3 K-tiles and N = 768 / 1536): epi 3 reads resid = hi + lo and writes
+    v = A W^T + b + resid as planes hi = bf16(v), lo = bf16(v - hi) plus the slab statistics; epi 4
+    writes v in f32.  vs torch f32: hi is the round-to-nearest bf16 of v, hi + lo within 2^-16 |v| of
+    v (f32 accumulation order aside)."""
+    L = _lib.lib()
     g = torch.Generator(device="cpu").manual_seed(M + K)
     A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
@@ -213,8 +224,16 @@ def test_gemm_ln_stats_hl(M, K):
     ns = N // 64
     outp = torch.full((2, M, N), 7.0, device=DEV, dtype=torch.bfloat16)
     part = torch.full((M, ns, 2), 7.0, device=DEV)
-    _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), None, _lib.CE_F32,
-              3, P(outp), P(part), None, None)
+    prev_v = L.ce_set_gemm_variant(-1)
+    L.ce_set_gemm_variant((prev_v & ~128) | (128 if rhl else 0))
+    try:
+        path_counts()
+        _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), None, _lib.CE_F32,
+                  3, P(outp), P(part), None, None)
+        cnt = path_counts()
+    finally:
+        L.ce_set_gemm_variant(prev_v)
+    assert cnt[0 + 1] == (1 if rhl else 0) and cnt[3 + 1] == (0 if rhl else 1), cnt     # W4PP / NT + LN stats
     out4 = torch.empty(M, N, device=DEV)
     _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), P(out4), _lib.CE_F32,
               4, None, None, None, None)

@@ -62,7 +62,9 @@ def main():
     # name: (N, K, act, epi, resid, out_bf16)
     shapes = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True, False),
               "fc": (4096, 1024, 1, 2, False, True), "proj": (1024, 4096, 0, 1, True, False),
-              "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True), "sq": (4096, 4096, 0, 0, False, True)}
+              "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True), "sq": (4096, 4096, 0, 0, False, True),
+              # hi/lo residual stream (epi 3: resid and xb are [2][M][N] bf16 planes, no f32 output)
+              "out_hl": (1024, 1024, 0, 3, True, False), "proj_hl": (1024, 4096, 0, 3, True, False)}
     if args.only:
         shapes = {k: v for k, v in shapes.items() if k in args.only.split(",")}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -81,9 +83,12 @@ def main():
         W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
         bias = torch.rand(N, device="cuda", generator=g)
         R = torch.rand(m, N, device="cuda", generator=g) if resid else None
-        O = torch.empty(m, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
+        O = torch.empty(m, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32) if epi != 3 else None
         xb = torch.empty(m, N, device="cuda", dtype=torch.bfloat16) if epi == 1 else None
-        part = torch.empty(m, N // 64, 2, device="cuda") if epi == 1 else None
+        part = torch.empty(m, N // 64, 2, device="cuda") if epi in (1, 3) else None
+        if epi == 3:
+            R = torch.stack([R.to(torch.bfloat16), torch.zeros(m, N, device="cuda", dtype=torch.bfloat16)]).contiguous()
+            xb = torch.empty(2, m, N, device="cuda", dtype=torch.bfloat16)
         st = torch.stack([torch.rand(m, device="cuda", generator=g) * 0.1,
                           torch.rand(m, device="cuda", generator=g) + 0.5], 1).contiguous() if epi == 2 else None
         fc = W.float().sum(1).contiguous() if epi == 2 else None

@@ -19,7 +19,8 @@ from bench_gemm_epi import P, parse  # noqa: E402
 
 SHAPES = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True, False),
           "fc": (4096, 1024, 1, 2, False, True), "proj": (1024, 4096, 0, 1, True, False),
-          "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True)}
+          "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True),
+          "out_hl": (1024, 1024, 0, 3, True, False), "proj_hl": (1024, 4096, 0, 3, True, False)}
 
 
 def main():
@@ -35,9 +36,12 @@ def main():
     W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
     bias = torch.rand(N, device="cuda", generator=g)
     R = torch.rand(M, N, device="cuda", generator=g) if resid else None
-    O = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
+    O = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if ob else torch.float32) if epi != 3 else None
     xb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi == 1 else None
-    part = torch.empty(M, N // 64, 2, device="cuda") if epi == 1 else None
+    part = torch.empty(M, N // 64, 2, device="cuda") if epi in (1, 3) else None
+    if epi == 3:     # hi/lo planes
+        R = torch.stack([R.to(torch.bfloat16), torch.zeros_like(R, dtype=torch.bfloat16)]).contiguous()
+        xb = torch.empty(2, M, N, device="cuda", dtype=torch.bfloat16)
     st = torch.stack([torch.rand(M, device="cuda", generator=g) * 0.1,
                       torch.rand(M, device="cuda", generator=g) + 0.5], 1).contiguous() if epi == 2 else None
     fc = W.float().sum(1).contiguous() if epi == 2 else None
