@@ -1756,6 +1756,7 @@ __device__ __forceinline__ float sum_lane_groups(float v) {
 //  * the next tile waits for its K-tile 0 with vmcnt(52): the 36 stores of (e) and the 16 DMAs of
 //    K-tile 1 may stay in flight.
 // Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.
+template <int ABL>      // ABL: timing ablations (bit 0 no residual loads, bit 1 no stores; wrong outputs)
 __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
@@ -1959,22 +1960,28 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         // opaque: hoisted, they would be spilled, and a scratch reload waits for every store)
         const __amdgpu_buffer_rsrc_t hs = make_srd(p.rhl + (size_t)mbase * ldr, rows * ldr * 2);
         const __amdgpu_buffer_rsrc_t ls = make_srd(p.rhl + p.hl_plane + (size_t)mbase * ldr, rows * ldr * 2);
-        const int ro = (fre * ldr + nbase + fqe * 4) * 2;
-        auto load_rows = [&](uint2 (&h)[2][8], uint2 (&l)[2][8], int i0) __attribute__((always_inline)) {
-            int io = i0 * 16 * ldr * 2, st = 16 * ldr * 2;
-            asm volatile("" : "+s"(io), "+s"(st));
+        constexpr bool abl_r = (ABL & 1) != 0, abl_s = (ABL & 2) != 0;
+        // a fragment-row pair (i0, i0 + 1) is loaded in the store layout (16 B = 8 columns of one
+        // row per lane, half the instructions of the 8-B fragment layout) and turned into fragments
+        // by the same v_permlane16_swap pairing that the stores use (an involution)
+        const int rp = ((fre + (fqe & 1) * 16) * ldr + nbase + (fqe >> 1) * 8) * 2;
+        auto load_pair = [&](u32x4 (&h)[8], u32x4 (&l)[8], int i0) __attribute__((always_inline)) {
+            if constexpr (abl_r) {                        // timing ablation: no residual loads
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int vo = ro + io + i * st;
+                for (int j = 0; j < 8; ++j) h[j] = l[j] = u32x4{0u, 0u, 0u, 0u};
+                return;
+            }
+            int io = i0 * 16 * ldr * 2;
+            asm volatile("" : "+s"(io));
+            const int vo = rp + io;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    h[i][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(hs, vo + j * 32, 0, 0));
-                    l[i][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ls, vo + j * 32, 0, 0));
-                }
+            for (int j = 0; j < 8; ++j) {
+                h[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(hs, vo + j * 32, 0, 0));
+                l[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ls, vo + j * 32, 0, 0));
             }
         };
-        uint2 rah[2][8], ral[2][8], rbh[2][8], rbl[2][8];
-        load_rows(rah, ral, 4);
+        u32x4 rah[8], ral[8], rbh[8], rbl[8];
+        load_pair(rah, ral, 4);
         const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
         const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
         int xo = ((fre + (fqe & 1) * 16) * ldo + nbase + (fqe >> 1) * 8) * 2;
@@ -1988,10 +1995,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 uint2 h[2], l[2];
+                float4 rr[2];
+                get_r(i0, j, rr);
 #pragma unroll
                 for (int r2 = 0; r2 < 2; ++r2) {
                     f32x4 v = acc[i0 + r2][j];
-                    const float4 r = get_r(i0 + r2, j);
+                    const float4 r = rr[r2];
                     v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
                     const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
                     const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
@@ -2014,8 +2023,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 const auto yy = __builtin_amdgcn_permlane16_swap(l[0].y, l[1].y, false, false);
                 const u32x4 dh = {x[0], y[0], x[1], y[1]};
                 const u32x4 dl = {xx[0], yy[0], xx[1], yy[1]};
-                __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
+                if constexpr (!abl_s) {                   // (timing ablation: no stores)
+                    __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
+                }
             }
             xo += 32 * ldo * 2;
 #pragma unroll
@@ -2036,19 +2047,22 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         // (b) fragment rows 0-3: residual from the staged planes
         const int lr0 = ((nk - 2) & 1) * STAGE_BYTES + (wm * 64 + fre) * 512;
         const int llo = (((nk - 1) & 1) - ((nk - 2) & 1)) * STAGE_BYTES;
-        auto lds_r = [&](int i, int j) {
+        auto lds_r = [&](int i0, int j, float4 (&rr)[2]) {
             const int c = (wn * 16 + 2 * j + (fqe >> 1)) ^ fre;        // staged row r has r & 15 == fre
-            const int off = lr0 + i * 16 * 512 + (c << 4) + (fqe & 1) * 8;
-            const uint2 h = *reinterpret_cast<const uint2*>(smem + off);
-            const uint2 l = *reinterpret_cast<const uint2*>(smem + llo + off);
-            const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
-            return make_float4(a.x, a.y, b.x, b.y);
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const int off = lr0 + (i0 + r2) * 16 * 512 + (c << 4) + (fqe & 1) * 8;
+                const uint2 h = *reinterpret_cast<const uint2*>(smem + off);
+                const uint2 l = *reinterpret_cast<const uint2*>(smem + llo + off);
+                const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
+                rr[r2] = make_float4(a.x, a.y, b.x, b.y);
+            }
         };
         row_pair(0, lds_r);
         asm volatile("" ::: "memory");          // rows 2-3's LDS reads stay behind rows 0-1 (VGPRs)
         row_pair(2, lds_r);
         // (a2) residual of rows 6-7 (behind the 32 stores of (b), ahead of the next tile's DMAs)
-        load_rows(rbh, rbl, 6);
+        load_pair(rbh, rbl, 6);
         // (c) every wave's LDS residual reads done -> (d) the next tile's bias and K-tiles 0 and 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier();
@@ -2063,10 +2077,17 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             for (int j = 0; j < 16; ++j) dma_k(1, 1, j, vA, vW);
         }
         // (e) fragment rows 4-7 from the registers of (a) and (a2)
-        auto reg_r = [&](int i, int j) {
-            const uint2 h = i < 6 ? rah[i - 4][j] : rbh[i - 6][j], l = i < 6 ? ral[i - 4][j] : rbl[i - 6][j];
-            const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
-            return make_float4(a.x, a.y, b.x, b.y);
+        auto reg_r = [&](int i0, int j, float4 (&rr)[2]) {
+            const u32x4 dh = i0 == 4 ? rah[j] : rbh[j], dl = i0 == 4 ? ral[j] : rbl[j];
+            const auto hx = __builtin_amdgcn_permlane16_swap(dh[0], dh[2], false, false);
+            const auto hy = __builtin_amdgcn_permlane16_swap(dh[1], dh[3], false, false);
+            const auto lx = __builtin_amdgcn_permlane16_swap(dl[0], dl[2], false, false);
+            const auto ly = __builtin_amdgcn_permlane16_swap(dl[1], dl[3], false, false);
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const float2 a = join_hl(hx[r2], lx[r2]), b = join_hl(hy[r2], ly[r2]);
+                rr[r2] = make_float4(a.x, a.y, b.x, b.y);
+            }
         };
         row_pair(4, reg_r);
         row_pair(6, reg_r);
@@ -2460,7 +2481,11 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.K >= 2 * BK && nwg >= 2 * num_cus()) {
             p.gm = gemm_groupm();
             p.stagger = gemm_stagger();
-            hipLaunchKernelGGL(gemm_w4_resid_hl, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
+            if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             count_path(GEMM_PATH_W4PP + EPI_LN_STATS);
             return hipGetLastError();
         }
