@@ -1819,10 +1819,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     // 512 B (256 columns), 16-B chunk c of row r at c ^ (r & 15)
     // (the row offset stays in voffset, where the descriptor clips it at row M; the column offset
     // n0 goes to soffset; per-instruction row offsets are opaque so they are not hoisted to VGPRs)
-    const int rpair = wave * 2 + (lane >> 5);                   // r & 7 of the staged row
-    const int vr0 = (lane >> 5) * (int)p.ldr * 2 + ((lane & 31) ^ rpair) * 16;
-    const int vr1 = (lane >> 5) * (int)p.ldr * 2 + ((lane & 31) ^ (rpair | 8)) * 16;
-    auto dma_r = [&](int buf, int plane, int j) {
+    // (vr0 / vr1: lane offsets of the even / odd instructions, from r_offsets at each use)
+    auto r_offsets = [&](int& vr0, int& vr1) {
+        const int ln = fresh_lane_id();
+        const int rpair = wave * 2 + (ln >> 5);                 // r & 7 of the staged row
+        vr0 = (ln >> 5) * (int)p.ldr * 2 + ((ln & 31) ^ rpair) * 16;
+        vr1 = (ln >> 5) * (int)p.ldr * 2 + ((ln & 31) ^ (rpair | 8)) * 16;
+    };
+    auto dma_r = [&](int buf, int plane, int j, int vr0, int vr1) {
         int lb = buf * STAGE_BYTES + wave * 2 * 512;
         int l2 = (int)p.ldr * 2;
         asm volatile("" : "+s"(lb), "+s"(l2));
@@ -1840,6 +1844,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
 
     f32x4 acc[8][8];
     bf16x8 a0[8], b0[8], a1[8], b1[8];
+    u32x4 rah[8], ral[8];                       // residual of fragment rows 4-5 (hi, lo planes)
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rah[j] = ral[j] = u32x4{0u, 0u, 0u, 0u};
+    }
 #define CE_MFMA_AGPR(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
     auto read_set0 = [&](const char* sb0) __attribute__((always_inline)) {
@@ -1876,7 +1885,15 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier();
-        // K-tile kt + 2, or for the last two K-tiles the residual planes, into this buffer
+        // K-tile kt + 2, or for the last two K-tiles the residual planes, into this buffer; MODE 1
+        // also loads the residual of fragment rows 4-5 into registers (16-B store layout, see
+        // load_pair), retired by the last K-tile's wait instead of inside the epilogue
+        int rpk = 0, vr0 = 0, vr1 = 0;
+        if constexpr (MODE >= 1) r_offsets(vr0, vr1);
+        if constexpr (MODE == 1) {
+            const int lnr = fresh_lane_id();
+            rpk = ((wm * 128 + 64 + (lnr & 15) + ((lnr >> 4) & 1) * 16) * (int)p.ldr + wn * 128 + (lnr >> 5) * 8) * 2;
+        }
 #pragma unroll
         for (int s2 = 0; s2 < 64; ++s2) {
             const int i = (s2 >> 3) & 3, j = s2 & 7;
@@ -1884,12 +1901,26 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             else CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
             if ((s2 & 3) == 3) {
                 if constexpr (MODE == 0) dma_k(buf, kt + 2, s2 >> 2, voffA, voffW);
-                else dma_r(buf, MODE - 1, s2 >> 2);
+                else dma_r(buf, MODE - 1, s2 >> 2, vr0, vr1);
+            }
+            if constexpr (MODE == 1 && (ABL & 1) == 0) {
+                if ((s2 & 3) == 1) {
+                    const int q = s2 >> 2;
+                    if (q < 8) rah[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdH, rpk + q * 32, n0 * 2, 0));
+                    else ral[q - 8] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdL, rpk + (q - 8) * 32, n0 * 2, 0));
+                }
             }
         }
-        if (wait_n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if (wait_n == 52) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (MODE == 1 && (ABL & 1) == 0) {
+            // 16 residual DMAs + 16 register loads younger than K-tile nk - 1 (+ the previous
+            // epilogue's 36 stores when nk == 2: 68 > 63, so the wait over-covers by 5)
+            if (wait_n == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+        } else {
+            if (wait_n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (wait_n == 52) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         barrier();
 #pragma unroll
         for (int s2 = 0; s2 < 32; ++s2) {
@@ -1956,8 +1987,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         const int lne = fresh_lane_id();
         const int fre = lne & 15, fqe = lne >> 4;
         const int rows = max(0, min(p.M - mbase, 128));
-        // (a) residual of fragment rows 4-5 into registers before any store (per-row offsets are
-        // opaque: hoisted, they would be spilled, and a scratch reload waits for every store)
+        // residual rows in registers (per-row offsets are opaque: hoisted, they would be spilled, and
+        // a scratch reload waits for every store)
         const __amdgpu_buffer_rsrc_t hs = make_srd(p.rhl + (size_t)mbase * ldr, rows * ldr * 2);
         const __amdgpu_buffer_rsrc_t ls = make_srd(p.rhl + p.hl_plane + (size_t)mbase * ldr, rows * ldr * 2);
         constexpr bool abl_r = (ABL & 1) != 0, abl_s = (ABL & 2) != 0;
@@ -1980,8 +2011,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 l[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ls, vo + j * 32, 0, 0));
             }
         };
-        u32x4 rah[8], ral[8], rbh[8], rbl[8];
-        load_pair(rah, ral, 4);
+        // (a) rows 6-7 (rows 4-5 arrived with the last K-tiles)
+        u32x4 rbh[8], rbl[8];
+        load_pair(rbh, rbl, 6);
         const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
         const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
         int xo = ((fre + (fqe & 1) * 16) * ldo + nbase + (fqe >> 1) * 8) * 2;
@@ -2061,8 +2093,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         row_pair(0, lds_r);
         asm volatile("" ::: "memory");          // rows 2-3's LDS reads stay behind rows 0-1 (VGPRs)
         row_pair(2, lds_r);
-        // (a2) residual of rows 6-7 (behind the 32 stores of (b), ahead of the next tile's DMAs)
-        load_pair(rbh, rbl, 6);
         // (c) every wave's LDS residual reads done -> (d) the next tile's bias and K-tiles 0 and 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier();
