@@ -1770,7 +1770,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     const int grid = gridDim.x;
     const int slot = xcd_remap(blockIdx.x, grid);
     const int nk = p.K / BK;
-    const int my_tiles = slot < nwg ? (nwg - 1 - slot) / grid + 1 : 0;
+    // tiles t_main..nwg-1 (a last round of <= grid/8 tiles) run as split-K chunks on the 4-phase
+    // kernel + gemm_splitk_fixup (plan_tail_rhl)
+    const int t_main = nwg - p.tail;
+    const int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
     // de-synchronised start (p.stagger x s_sleep 127 for the odd slots): equal tiles keep the CUs in
     // lock-step, K-loops (MFMA-bound) and epilogues (HBM-bound) each chip-wide at once
     if (p.stagger > 0 && (slot & 1))
@@ -2423,6 +2426,22 @@ void plan_tail_w4(GemmParams& p, int nwg, int grid) {
     p.split = S;
 }
 
+// Split-K tail of the staged-residual kernel (default on with split-K): a last round of r <= grid/8
+// tiles (B = 256: 2308 tiles = 9 x 256 + 4) would hold one tile period (c_proj ~135 us) for r CUs;
+// those tiles run as S K-chunks on the 4-phase kernel instead (tail_only) + the hi/lo fixup
+void plan_tail_rhl(GemmParams& p, int nwg, int grid) {
+    p.tail = 0;
+    p.split = 1;
+    if (!splitk_enabled() || !p.part) return;
+    const int r = nwg % grid, nk = p.K / BK;
+    if (nwg < grid || r == 0 || r > grid / 8) return;
+    int S = std::min(std::min(std::max(nk / 4, 2), 16), std::min(grid / r, nk));
+    while (S >= 2 && (long)r * S * BM * BN > p.part_elems) --S;
+    if (S < 2) return;
+    p.tail = r;
+    p.split = S;
+}
+
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
 // (GEMM_VAR_W4_ONETILE: one workgroup per tile)
 int w4pp_grid(int nwg) {
@@ -2511,12 +2530,22 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.K >= 2 * BK && nwg >= 2 * num_cus()) {
             p.gm = gemm_groupm();
             p.stagger = gemm_stagger();
+            plan_tail_rhl(p, nwg, w4pp_grid(nwg));
             const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
             if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             count_path(GEMM_PATH_W4PP + EPI_LN_STATS);
+            if (p.tail > 0) {
+                GemmParams q = p;
+                q.tail_only = 1;
+                hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, true, false, 1, 3, EPI_LN_STATS_HL>), dim3(p.tail * p.split),
+                                   dim3(NTHREADS), 0, s, q);
+                hipLaunchKernelGGL((gemm_splitk_fixup<ACT_NONE, true, false, EPI_LN_STATS_HL>), dim3(p.tail * 64),
+                                   dim3(256), 0, s, p);
+                count_path(GEMM_PATH_FIXUP + EPI_LN_STATS);
+            }
             return hipGetLastError();
         }
     }

@@ -234,6 +234,9 @@ def test_gemm_ln_stats_hl(M, K, N, rhl):
     finally:
         L.ce_set_gemm_variant(prev_v)
     assert cnt[0 + 1] == (1 if rhl else 0) and cnt[3 + 1] == (0 if rhl else 1), cnt     # W4PP / NT + LN stats
+    if rhl:      # split-K tail of a last round of <= 32 tiles (M = 147,712: 2308 = 9 x 256 + 4)
+        nwg = -(-M // 256) * (N // 256)
+        assert cnt[6 + 1] == (1 if 0 < nwg % 256 <= 32 else 0), cnt
     out4 = torch.empty(M, N, device=DEV)
     _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), P(out4), _lib.CE_F32,
               4, None, None, None, None)
