@@ -16,7 +16,9 @@ import sys
 KERNEL = {"attn_v": "attn_fwd", "attn_t": "attn_fwd", "ln_v": "layernorm_k"}
 # tools/pmc_traffic2.sh shapes (bench_gemm_epi names): the main GEMM kernel of the launch (the
 # persistent four-wave kernel for qkv / fc, the 4-phase kernel for out / proj)
-KERNEL2 = {"qkv": "gemm_bf16_w4pp", "fc": "gemm_bf16_w4pp", "out": "gemm_bf16_nt", "proj": "gemm_bf16_nt"}
+KERNEL2 = {"qkv": "gemm_bf16_w4pp", "fc": "gemm_bf16_w4pp", "out": "gemm_bf16_nt", "proj": "gemm_bf16_nt",
+           # the hi/lo residual GEMMs on the staged-residual four-wave kernel (default since r02)
+           "out_hl": "gemm_w4_resid_hl", "proj_hl": "gemm_w4_resid_hl"}
 
 
 def avg_counter(d, counter, kname):
@@ -32,6 +34,9 @@ def avg_counter(d, counter, kname):
 def main():
     root, out = sys.argv[1], sys.argv[2]
     res = {}
+    if os.path.exists(out):          # merge: keep the entries of shapes not measured in this run
+        with open(out) as f:
+            res = json.load(f)
     shapes = sorted({os.path.basename(p).rsplit("_", 2)[0] for p in glob.glob(os.path.join(root, "*_FETCH_SIZE"))})
     for s in shapes:
         kname = KERNEL.get(s, KERNEL2.get(s, "gemm_bf16_nt"))
