@@ -308,6 +308,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--serial-towers", action="store_true", help="clip: both towers on one stream")
     ap.add_argument("--tower-priority", action="store_true", help="clip: image tower on a high-priority stream")
+    ap.add_argument("--attn-var", type=int, default=-1, help="attention forward variant for A/B (-1 = default)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -323,6 +324,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
+    if args.attn_var >= 0:
+        from clipembed import _lib
+        _lib.lib().ce_set_attn_variant(args.attn_var)
     t0 = time.time()
     W = BUILDERS[args.workload](args, dev, rank, world)
     engine, step = W["engine"], W["step"]

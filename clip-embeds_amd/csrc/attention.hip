@@ -21,6 +21,8 @@
 //  * K tile LDS image swizzled (16-B chunk c of row r at c ^ ((r>>1)&7)) for conflict-free
 //    ds_read_b128; ragged tails (L = 577 = 9*64 + 1, L = 77) are clamped on load and masked
 //    with -inf in the scores.
+#include <type_traits>
+
 #include "ce_device.h"
 #include "ce_kernels.h"
 
@@ -42,7 +44,15 @@ __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <bool CAUSAL>
+// Variants (set_attn_variant): 0 = every tile on the general online-softmax path;
+// 1 = "fixed-offset" tiles: once tile 0 has shown every row max of the wave within +-64 (log2
+// units), the softmax offset stays 0 and full tiles skip the row max, the accumulator moves and
+// the subtraction (p = exp2(q.k) directly; bf16 P has the f32 exponent range, O and l the same
+// factor), with an overflow check on the row sums (any p > 2^64 or inf/NaN: the tile is redone
+// with the exact max and the wave returns to the general path); 2 = as 1, with the row sums of
+// the fast tiles taken by the MFMA (a ones A operand beside the P.V products: l^T = 1 P^T) and
+// the overflow check on a max3 reduction of the scores.
+template <bool CAUSAL, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int L, int H,
                                                     float qscale, float* __restrict__ lse) {
@@ -130,19 +140,63 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     f32x16 o[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+    // VAR 2: row sums of the fast tiles, l^T = 1 . P^T (every entry of a lane = its query's sum
+    // over both key halves; entry 0 is read)
+    f32x16 lm;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lm[i] = 0.f;
+    bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
     float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
     float l_run = 0.f;   // partial (this half's keys)
+    bool fast = false;   // wave-uniform: softmax offset fixed at 0 (VAR >= 1)
+    const f32x16 zero16 = {};
+
+    // O^T += V^T P^T for the tile's P fragments (pf[kt2][s2]: keys kt2*32 + 16*s2 .. +15)
+    auto pv = [&](const char* vb, const bf16x8 (&pf)[2][2], bool with_half2, bool rowsum) {
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                if (kt2 == 1 && !with_half2) continue;
+                const int krow = kt2 * 32 + 16 * s2;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    const char* a0 = vb + krow * 128 + voff[dt];
+                    const s16x4 lo = ds_read_tr16(a0);
+                    const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
+                    typedef __attribute__((ext_vector_type(8))) short s16x8;
+                    const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
+                }
+                if (rowsum) lm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kt2][s2], lm, 0, 0, 0);
+            }
+    };
+    // rescale of O and l by 2^-delta (delta per lane, equal on lanes l and l^32)
+    auto rescale = [&](float delta) {
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        l_run *= alpha;
+        lm[0] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        m_run += delta;
+    };
 
     stage(0, 0);
-    for (int t = 0; t < nkt; ++t) {
+    // one key tile; BUF (the ring slot, t & 1) is a compile-time constant so every LDS address
+    // is a per-lane offset plus an immediate (the loop is unrolled by two)
+    auto tile = [&](const int t, auto bufc) {
+        constexpr int BUF = decltype(bufc)::value;
         if (t + 1 < nkt) {
-            stage(t + 1, (t + 1) & 1);
+            stage(t + 1, BUF ^ 1);
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();
-        const char* kb = smem + (t & 1) * STAGE_BYTES;
+        const char* kb = smem + BUF * STAGE_BYTES;
         const char* vb = kb + TILE_KV_BYTES;
 
         // waves whose queries are all padding, or (causal) whose queries all precede this key
@@ -151,7 +205,73 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         // second 32-key subtile entirely past the sequence end (L = 577: the last tile holds one
         // key) or (causal) entirely above this wave's diagonal: skip its MFMAs and exponentials
         const bool half2 = (t * KBLK + 32 < L) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
-        if (active) {
+        const int key0 = t * KBLK;
+        // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
+        const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
+        const bool fast_tile = VAR >= 1 && fast && half2 && !need_mask;   // wave-uniform
+        bool redo = false;
+        if (active && fast_tile) {
+            // ---- fixed-offset tile: S^T = K Q^T from a zero accumulator, p = exp2(s) ----
+            f32x16 s[2];
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                    s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? zero16 : s[kt2], 0, 0, 0);
+                }
+            bool overflow;
+            float psum = 0.f;
+            bf16x8 pf[2][2];
+            if (VAR == 2) {
+                // overflow check on the scores themselves (the sums come from the MFMA)
+                float mx[2];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2) {
+                    float a = s[kt2][0];
+#pragma unroll
+                    for (int i = 1; i < 16; i += 2) a = fmaxf(a, fmaxf(s[kt2][i], s[kt2][i + 1]));
+                    mx[kt2] = a;
+                }
+                // !(x <= 64) also catches NaN
+                overflow = __any(!(fmaxf(mx[0], mx[1]) <= 64.0f));
+            } else {
+                float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                            ps[j & 3] += pv_;
+                            pf[kt2][s2][j] = (__bf16)pv_;
+                        }
+                psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+                overflow = __any(!(psum <= 0x1p64f));
+            }
+            if (!overflow) {
+                if (VAR == 2) {
+#pragma unroll
+                    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                pf[kt2][s2][j] = (__bf16)__builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                } else {
+                    l_run += psum;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                pv(vb, pf, true, VAR == 2);
+            } else {
+                // rare: the tile is redone on the general path below (exact row max, rescale),
+                // and the wave stays there
+                fast = false;
+                redo = true;
+            }
+        }
+        if (active && (redo || !(VAR >= 1 && fast_tile))) {
             // ---- S^T = K Q^T (two 32-key subtiles) ----
             f32x16 s[2];
     #pragma unroll
@@ -168,9 +288,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 
             // ---- online softmax, log2 domain.  The S accumulator starts at -m_run, so the MFMA
             // leaves s = q.k - m_run (q pre-scaled): p = exp2(s) needs no per-score FMA ----
-            const int key0 = t * KBLK;
-            // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
-            const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
             if (need_mask) {
     #pragma unroll
                 for (int kt2 = 0; kt2 < 2; ++kt2)
@@ -189,18 +306,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));    // relative to m_run
             // Deferred rescale (guide T13): m_run moves on the first tile (to the exact row max:
             // key 0 is never masked, so it is finite) and afterwards only when a row max exceeds
-            // it by more than 8, so p <= 2^8 (exact range for the f32 sums and bf16 P) and O / l
-            // are rarely rescaled.  O and l always see the same factor, and the decision precedes
-            // this tile's P, so no P.V product straddles it.
-            if (t == 0 || __any(tmax > 8.0f)) {
+            // it by more than the threshold (8, or 64 with the offset fixed at 0), so p stays far
+            // from the f32 / bf16 overflow and O / l are rarely rescaled.  O and l always see the
+            // same factor, and the decision precedes this tile's P, so no P.V product straddles it.
+            // VARs >= 1: when tile 0's row maxima all lie within +-64, the offset stays 0.
+            const bool fix0 = VAR >= 1 && t == 0 && __all(tmax <= 64.0f && tmax >= -64.0f);
+            if (fix0) fast = true;
+            if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
                 const float delta = t == 0 ? tmax : fmaxf(tmax, 0.f);
-                if (t != 0) {
-                    const float alpha = __builtin_amdgcn_exp2f(-delta);
-                    l_run *= alpha;
-    #pragma unroll
-                    for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-                }
-                m_run += delta;
+                if (t != 0) rescale(delta);
+                else m_run += delta;
+                fast = false;
     #pragma unroll
                 for (int kt2 = 0; kt2 < 2; ++kt2)
     #pragma unroll
@@ -215,37 +331,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         if (kt2 == 1 && !half2) { pf[kt2][s2][j] = (__bf16)0.f; continue; }
-                        const float pv = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
-                        psum += pv;
-                        pf[kt2][s2][j] = (__bf16)pv;
+                        const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                        psum += pv_;
+                        pf[kt2][s2][j] = (__bf16)pv_;
                     }
             l_run += psum;
-
-            // ---- O^T += V^T P^T ----
-    #pragma unroll
-            for (int kt2 = 0; kt2 < 2; ++kt2)
-    #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    if (kt2 == 1 && !half2) continue;
-                    const int krow = kt2 * 32 + 16 * s2;
-    #pragma unroll
-                    for (int dt = 0; dt < 2; ++dt) {
-                        const char* a0 = vb + krow * 128 + voff[dt];
-                        const s16x4 lo = ds_read_tr16(a0);
-                        const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
-                        typedef __attribute__((ext_vector_type(8))) short s16x8;
-                        const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                        const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
-                    }
-                }
+            pv(vb, pf, half2, false);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier();
+    };
+    for (int t = 0; t < nkt; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
     }
 
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (VAR == 2 ? lm[0] : 0.f);
     const float inv = 1.0f / l_tot;
     // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
     if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * L + qrow] = m_run + __log2f(l_tot);
@@ -264,6 +366,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     }
 }
 
+int g_attn_var = 1;
+
 }  // namespace
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
@@ -271,11 +375,25 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
-    if (causal)
-        hipLaunchKernelGGL(attn_fwd<true>, grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse);
-    else
-        hipLaunchKernelGGL(attn_fwd<false>, grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse);
+#define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse)
+    if (causal) {
+        // the text tower's causal tiles all cross the diagonal or the ragged end: general path
+        CE_ATTN_LAUNCH(true, 0);
+    } else if (g_attn_var == 2) {
+        CE_ATTN_LAUNCH(false, 2);
+    } else if (g_attn_var == 1) {
+        CE_ATTN_LAUNCH(false, 1);
+    } else {
+        CE_ATTN_LAUNCH(false, 0);
+    }
+#undef CE_ATTN_LAUNCH
     return hipGetLastError();
+}
+
+int set_attn_variant(int var) {
+    const int prev = g_attn_var;
+    g_attn_var = (var >= 0 && var <= 2) ? var : 1;
+    return prev;
 }
 
 }  // namespace ce

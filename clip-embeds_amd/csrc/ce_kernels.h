@@ -75,6 +75,7 @@ constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a 
 // q_prescaled: the q third of qkv already carries kAttnQScale (engine in_proj weights); else the
 // kernel scales its Q fragments.
 constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(64)
+int set_attn_variant(int var);  // attention forward variant (0-2) for A/B; returns previous
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse = nullptr);   // lse: [B][H][L] log2 log-sum-exp (training)
 

@@ -274,6 +274,12 @@ int ce_set_gemm_auto(int mode);
  * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
+/* Attention-forward variant for A/B, non-causal launches only: 0 = every key tile
+ * on the general online-softmax path (row max, offset accumulators, deferred rescale); 1 (default)
+ * = fixed-offset tiles once tile 0's row maxima lie within +-64 (log2 units): no row max, no
+ * offset, overflow-checked row sums; 2 = as 1 with the row sums taken by the MFMA.  Out-of-range
+ * values restore the default.  Returns the previous variant. */
+int ce_set_attn_variant(int var);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
  * schedules, 10 = two-workgroup 256 x 128 (SCHED 12), and epi 0 = plain, 1 = LN statistics, 2 = LN

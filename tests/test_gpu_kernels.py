@@ -279,19 +279,37 @@ def attn_ref(qkv, B, L, H, causal):
 @pytest.mark.parametrize("B,L,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1, 16, False),
                                           (2, 64, 4, False), (2, 65, 4, True), (1, 129, 2, False),
                                           (1, 300, 12, True), (5, 577, 1, False)])
-def test_attention(B, L, H, causal):
-    g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
-    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16).to(DEV)
+@pytest.fixture(params=[0, 1, 2], ids=["attn_var0", "attn_var1", "attn_var2"])
+def attn_var(request):
+    """Every attention forward variant (ce_set_attn_variant) against torch f32."""
+    prev = _lib.lib().ce_set_attn_variant(request.param)
+    yield request.param
+    _lib.lib().ce_set_attn_variant(prev)
+
+
+def run_attn(qkv, B, L, H, causal):
     out = torch.empty(B * L, H * 64, device=DEV, dtype=torch.bfloat16)
     _lib.call("ce_kernel_attention", S(), P(qkv), P(out), B, L, H, 1 if causal else 0)
     torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("B,L,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1, 16, False),
+                                          (2, 64, 4, False), (2, 65, 4, True), (1, 129, 2, False),
+                                          (1, 300, 12, True), (5, 577, 1, False)])
+def test_attention(B, L, H, causal, attn_var):
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16).to(DEV)
+    out = run_attn(qkv, B, L, H, causal)
     ref = attn_ref(qkv, B, L, H, causal)
     err = (out.float() - ref).abs().max().item()
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
 
 
-def test_attention_spike_rescale():
-    """Force the online-softmax rescale: a late key dominates one query (guide §5.4 rule 26)."""
+def test_attention_spike_rescale(attn_var):
+    """Force the online-softmax rescale: a late key dominates one query (guide §5.4 rule 26).  On
+    the fixed-offset variants the score (~184 in log2 units) overflows the fast tile's check, so
+    the tile is redone with the exact max and the wave returns to the general path."""
     B, L, H = 1, 577, 2
     g = torch.Generator(device="cpu").manual_seed(3)
     qkv = torch.randn(B * L, 3 * H * 64, generator=g) * 0.5
@@ -299,11 +317,51 @@ def test_attention_spike_rescale():
     qkv[10, 0:64] = 4.0                 # query 10, head 0
     qkv[500, D:D + 64] = 4.0            # key 500 -> huge score for query 10 at the 8th key tile
     qkv = qkv.to(torch.bfloat16).to(DEV)
-    out = torch.empty(B * L, D, device=DEV, dtype=torch.bfloat16)
-    _lib.call("ce_kernel_attention", S(), P(qkv), P(out), B, L, H, 0)
-    torch.cuda.synchronize()
+    out = run_attn(qkv, B, L, H, False)
     ref = attn_ref(qkv, B, L, H, False)
     assert (out.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("key", [3, 100, 576])
+def test_attention_spike_positions(key, attn_var):
+    """A dominant key in tile 0 (row max > 64: the wave never takes the fixed offset), inside a
+    fast tile (overflow redo), and the single-key last tile (general path with a fixed offset)."""
+    B, L, H = 2, 577, 2
+    g = torch.Generator(device="cpu").manual_seed(key)
+    qkv = torch.randn(B * L, 3 * H * 64, generator=g) * 0.5
+    D = H * 64
+    for q in (5, 200, 570):
+        qkv[q, 0:64] = 4.0
+    qkv[L + 7, 64:128] = -4.0
+    qkv[key, D:D + 64] = 4.0
+    qkv[L + key, D + 64:D + 128] = -4.0
+    qkv = qkv.to(torch.bfloat16).to(DEV)
+    out = run_attn(qkv, B, L, H, False)
+    ref = attn_ref(qkv, B, L, H, False)
+    assert (out.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("scale", [3.0, 4.5])
+def test_attention_wide_scores(scale, attn_var):
+    """Scores spread over tens of log2 units (p up to ~2^60 on the fixed offset, no overflow), and
+    beyond (scale 4.5: some rows overflow the check)."""
+    B, L, H = 2, 577, 4
+    g = torch.Generator(device="cpu").manual_seed(int(scale * 10))
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    out = run_attn(qkv, B, L, H, False)
+    ref = attn_ref(qkv, B, L, H, False)
+    # the bf16 rounding of the pre-scaled q moves scores of ~100 log2 units by ~0.2: near-one-hot
+    # rows at scale 4.5 sit at a few % of max|O| against f32 torch on any variant
+    tol = 2e-2 if scale < 4 else 6e-2
+    err = (out.float() - ref).abs().max().item()
+    assert err < tol * max(1.0, ref.abs().max().item()), err
+    prev = _lib.lib().ce_set_attn_variant(0)
+    try:
+        base = run_attn(qkv, B, L, H, False)
+    finally:
+        _lib.lib().ce_set_attn_variant(prev)
+    err0 = (out.float() - base.float()).abs().max().item()
+    assert err0 < 2e-2 * max(1.0, ref.abs().max().item()), err0
 
 
 @pytest.mark.parametrize("rows,D,bf16", [(1000, 1024, True), (1000, 1024, False), (77, 768, True), (3, 768, False)])

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--warm-s", type=float, default=2.0)
     ap.add_argument("--torch-ref", action="store_true", help="also time torch.matmul (hipBLASLt) per shape")
     ap.add_argument("--only", default="", help="comma list of shape names to run (default all)")
+    ap.add_argument("--attn-vars", default="1", help="comma list of attention variants (ce_set_attn_variant) to A/B")
     args = ap.parse_args()
     B = args.batch
     Mv, Mt = B * 577, B * 77
@@ -113,8 +114,12 @@ def main():
         qkv = (torch.randn(Bx * L, 3 * H * 64, device="cuda", generator=g)).to(torch.bfloat16)
         out = torch.empty(Bx * L, H * 64, device="cuda", dtype=torch.bfloat16)
         for rnd in range(args.rounds):
-            ms = timeit(lambda: _lib.call("ce_kernel_attention", stream, P(qkv), P(out), Bx, L, H, causal), args.reps)
-            res.setdefault(attn, []).append(4.0 * Bx * H * L * L * 64 / (ms * 1e-3) / 1e12)
+            for var in [int(v) for v in args.attn_vars.split(",")]:
+                _lib.lib().ce_set_attn_variant(var)
+                ms = timeit(lambda: _lib.call("ce_kernel_attention", stream, P(qkv), P(out), Bx, L, H, causal),
+                            args.reps)
+                res.setdefault(f"{attn}/var{var}", []).append(4.0 * Bx * H * L * L * 64 / (ms * 1e-3) / 1e12)
+        _lib.lib().ce_set_attn_variant(-1)
     for rows, D in (((Mv, 1024),) if not args.only or "ln_v" in keep else ()):
         x = torch.randn(rows, D, device="cuda", generator=g)
         w = torch.ones(D, device="cuda")
