@@ -57,6 +57,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                                                     bf16_t* __restrict__ out, int L, int H,
                                                     float qscale, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
+    constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
+    constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
     float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
     float l_run = 0.f;   // partial (this half's keys)
-    bool fast = false;   // wave-uniform: softmax offset fixed at 0 (VAR >= 1)
+    bool fast = false;   // wave-uniform: softmax offset fixed at 0 (MODE >= 1)
     const f32x16 zero16 = {};
 
     // O^T += V^T P^T for the tile's P fragments (pf[kt2][s2]: keys kt2*32 + 16*s2 .. +15)
@@ -189,13 +192,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     // is a per-lane offset plus an immediate (the loop is unrolled by two)
     auto tile = [&](const int t, auto bufc) {
         constexpr int BUF = decltype(bufc)::value;
-        if (t + 1 < nkt) {
-            stage(t + 1, BUF ^ 1);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (ONEBAR) {
+            // tile t landed (the only DMA in flight) and every wave is done with tile t-1, whose
+            // slot BUF^1 then takes tile t+1
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            barrier();
+            if (t + 1 < nkt) stage(t + 1, BUF ^ 1);
         } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t + 1 < nkt) {
+                stage(t + 1, BUF ^ 1);
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            barrier();
         }
-        barrier();
         const char* kb = smem + BUF * STAGE_BYTES;
         const char* vb = kb + TILE_KV_BYTES;
 
@@ -208,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         const int key0 = t * KBLK;
         // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
         const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
-        const bool fast_tile = VAR >= 1 && fast && half2 && !need_mask;   // wave-uniform
+        const bool fast_tile = MODE >= 1 && fast && half2 && !need_mask;   // wave-uniform
         bool redo = false;
         if (active && fast_tile) {
             // ---- fixed-offset tile: S^T = K Q^T from a zero accumulator, p = exp2(s) ----
@@ -223,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             bool overflow;
             float psum = 0.f;
             bf16x8 pf[2][2];
-            if (VAR == 2) {
+            if (MODE == 2) {
                 // overflow check on the scores themselves (the sums come from the MFMA)
                 float mx[2];
 #pragma unroll
@@ -251,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 overflow = __any(!(psum <= 0x1p64f));
             }
             if (!overflow) {
-                if (VAR == 2) {
+                if (MODE == 2) {
 #pragma unroll
                     for (int kt2 = 0; kt2 < 2; ++kt2)
 #pragma unroll
@@ -263,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                     l_run += psum;
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                pv(vb, pf, true, VAR == 2);
+                pv(vb, pf, true, MODE == 2);
             } else {
                 // rare: the tile is redone on the general path below (exact row max, rescale),
                 // and the wave stays there
@@ -271,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 redo = true;
             }
         }
-        if (active && (redo || !(VAR >= 1 && fast_tile))) {
+        if (active && (redo || !(MODE >= 1 && fast_tile))) {
             // ---- S^T = K Q^T (two 32-key subtiles) ----
             f32x16 s[2];
     #pragma unroll
@@ -310,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             // from the f32 / bf16 overflow and O / l are rarely rescaled.  O and l always see the
             // same factor, and the decision precedes this tile's P, so no P.V product straddles it.
             // VARs >= 1: when tile 0's row maxima all lie within +-64, the offset stays 0.
-            const bool fix0 = VAR >= 1 && t == 0 && __all(tmax <= 64.0f && tmax >= -64.0f);
+            const bool fix0 = MODE >= 1 && t == 0 && __all(tmax <= 64.0f && tmax >= -64.0f);
             if (fix0) fast = true;
             if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
                 const float delta = t == 0 ? tmax : fmaxf(tmax, 0.f);
@@ -338,8 +349,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             l_run += psum;
             pv(vb, pf, half2, false);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        barrier();
+        if (!ONEBAR) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier();
+        }
     };
     for (int t = 0; t < nkt; t += 2) {
         tile(t, std::integral_constant<int, 0>{});
@@ -347,12 +360,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     }
 
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (VAR == 2 ? lm[0] : 0.f);
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (MODE == 2 ? lm[0] : 0.f);
     const float inv = 1.0f / l_tot;
     // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
     if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * L + qrow] = m_run + __log2f(l_tot);
-    if (qrow < L) {
-        bf16_t* op = out + ((size_t)b * L + qrow) * D + h * 64;
+    bf16_t* op = out + ((size_t)b * L + min(qrow, L - 1)) * D + h * 64;
+    if (WIDE) {
+        // lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
+        // trades the lower lane's odd-g words for the upper lane's even-g words, so each lane
+        // stores 8 consecutive d (16 B): the lower lane d = 16gp + 0..7, the upper 16gp + 8..15
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp) {
+                const int g0 = 2 * gp, g1 = 2 * gp + 1;
+                const uint32_t ax = pack_bf2(o[dt][4 * g0 + 0] * inv, o[dt][4 * g0 + 1] * inv);
+                const uint32_t ay = pack_bf2(o[dt][4 * g0 + 2] * inv, o[dt][4 * g0 + 3] * inv);
+                const uint32_t bx = pack_bf2(o[dt][4 * g1 + 0] * inv, o[dt][4 * g1 + 1] * inv);
+                const uint32_t by = pack_bf2(o[dt][4 * g1 + 2] * inv, o[dt][4 * g1 + 3] * inv);
+                const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                if (qrow < L)
+                    *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
+            }
+    } else if (qrow < L) {
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -366,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     }
 }
 
-int g_attn_var = 1;
+int g_attn_var = 13;
 
 }  // namespace
 
@@ -376,15 +407,20 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
 #define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse)
+    // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
+    const int v = g_attn_var;
     if (causal) {
-        // the text tower's causal tiles all cross the diagonal or the ragged end: general path
-        CE_ATTN_LAUNCH(true, 0);
-    } else if (g_attn_var == 2) {
-        CE_ATTN_LAUNCH(false, 2);
-    } else if (g_attn_var == 1) {
-        CE_ATTN_LAUNCH(false, 1);
+        if (v & 8) CE_ATTN_LAUNCH(true, 8); else CE_ATTN_LAUNCH(true, 0);
     } else {
-        CE_ATTN_LAUNCH(false, 0);
+        switch (v) {
+            case 0: CE_ATTN_LAUNCH(false, 0); break;
+            case 2: CE_ATTN_LAUNCH(false, 2); break;
+            case 5: CE_ATTN_LAUNCH(false, 5); break;
+            case 9: CE_ATTN_LAUNCH(false, 9); break;
+            case 13: CE_ATTN_LAUNCH(false, 13); break;
+            case 1: CE_ATTN_LAUNCH(false, 1); break;
+            default: CE_ATTN_LAUNCH(false, 13); break;
+        }
     }
 #undef CE_ATTN_LAUNCH
     return hipGetLastError();
@@ -392,7 +428,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
-    g_attn_var = (var >= 0 && var <= 2) ? var : 1;
+    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13) ? var : 13;
     return prev;
 }
 

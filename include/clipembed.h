@@ -274,11 +274,13 @@ int ce_set_gemm_auto(int mode);
  * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
-/* Attention-forward variant for A/B, non-causal launches only: 0 = every key tile
- * on the general online-softmax path (row max, offset accumulators, deferred rescale); 1 (default)
- * = fixed-offset tiles once tile 0's row maxima lie within +-64 (log2 units): no row max, no
- * offset, overflow-checked row sums; 2 = as 1 with the row sums taken by the MFMA.  Out-of-range
- * values restore the default.  Returns the previous variant. */
+/* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key tile
+ * on the general online-softmax path: row max, offset accumulators, deferred rescale; 1 = fixed-offset
+ * tiles once tile 0's row maxima lie within +-64 log2 units: no row max, no offset, overflow-checked
+ * row sums, an overflowing tile redone on the general path; 2 = as 1 with the row sums taken by the
+ * MFMA), 4 = one barrier per key tile, 8 = 16-B output stores.  Selectable: 0, 1, 2, 5, 9, 13
+ * (default); anything else restores the default.  Causal launches (text tower) use mode 0 with bit 8
+ * when set.  Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other

@@ -279,7 +279,7 @@ def attn_ref(qkv, B, L, H, causal):
 @pytest.mark.parametrize("B,L,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1, 16, False),
                                           (2, 64, 4, False), (2, 65, 4, True), (1, 129, 2, False),
                                           (1, 300, 12, True), (5, 577, 1, False)])
-@pytest.fixture(params=[0, 1, 2], ids=["attn_var0", "attn_var1", "attn_var2"])
+@pytest.fixture(params=[0, 1, 2, 5, 9, 13], ids=lambda v: f"attn_var{v}")
 def attn_var(request):
     """Every attention forward variant (ce_set_attn_variant) against torch f32."""
     prev = _lib.lib().ce_set_attn_variant(request.param)
