@@ -123,9 +123,18 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        // timing ablation of the LN-statistics epilogues: no bf16 copy of the output (wrong xb)
        GEMM_VAR_ABL_NOXB = 64,
        // the hi/lo residual GEMMs (EPI_LN_STATS_HL) on the staged-residual four-wave kernel
-       GEMM_VAR_W4_RHL = 128 };
+       GEMM_VAR_W4_RHL = 128,
+       // four-wave persistent schedule: a K-tile's 16 operand DMAs spread over B2 and B3 (one per
+       // ~6 MFMAs) instead of one per 4 MFMAs of B2 only
+       GEMM_VAR_W4_DMA_SPREAD = 256,
+       // the same spread on the staged-residual kernel's operand K-tiles
+       GEMM_VAR_RHL_DMA_SPREAD = 512,
+       // split of the spread four-wave schedule's 16 DMAs between B2 and B3: 12 + 4 or 8 + 8
+       // (default 10 + 6)
+       GEMM_VAR_W4_SPREAD12 = 1024, GEMM_VAR_W4_SPREAD8 = 2048 };
 #ifndef CE_GEMM_VAR_DEFAULT
-#define CE_GEMM_VAR_DEFAULT (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL)
+#define CE_GEMM_VAR_DEFAULT \
+    (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD)
 #endif
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
@@ -1481,9 +1490,16 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4p(GemmParams p) {
 // tiles a workgroup owns (grid = one workgroup per CU; tile r*grid + xcd_remap(b) in round r).
 // The DMA two K-tiles ahead runs into the next tile's first K-tiles, so the next tile's
 // operands are in flight while this tile's epilogue runs and there is no per-tile prologue.
+// EV bit 0: epilogue for one wave per SIMD with the side area (GEMM_VAR_W4_EPI2); bit 1: DMA
+// spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD)
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN, int EV = 0>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
-    constexpr bool SIDE = EV == 1;
+    constexpr bool SIDE = (EV & 1) != 0;
+    constexpr bool SPREAD = (EV & 2) != 0;
+    // DMAs of a K-tile issued in B2 (the rest in B3); the B2 wait leaves exactly these in flight
+    constexpr int DMA_B2 = !SPREAD ? 16 : (EV & 4) ? 12 : (EV & 8) ? 8 : 10;
+    constexpr int P2 = 64 / DMA_B2;                          // MFMAs per DMA in B2
+    constexpr int P3 = DMA_B2 < 16 ? 32 / (16 - DMA_B2) : 32; // and in B3
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + (SIDE ? 4 * W4_SIDE_BYTES : 0)];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1589,7 +1605,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     // first K-tile of a tile (EV 1): C = 0 instead of zeroing 256 accumulators per tile
 #define CE_MFMA_AGPR0(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(BV), "v"(AV))
-    constexpr bool NEWLOOP = EV == 1;
+    constexpr bool NEWLOOP = SIDE;
     // K-tile phases.  ZERO: first K-tile of a tile (C = 0 on each accumulator's first MFMA).
     // B3's PRE: read set0 of the next K-tile under its MFMAs; with EV 1 the last K-tile of a tile
     // does not (the next tile's set0 is read after the epilogue, so the epilogue has those 64
@@ -1617,14 +1633,21 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             } else {
                 CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
             }
-            if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
+            if constexpr (SPREAD) {
+                if (s2 % P2 == P2 - 1 && s2 / P2 < DMA_B2) dma(buf, s2 / P2, live);
+            } else {
+                if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
+            }
         }
     };
-    auto B3 = [&](const char* so, auto pre) __attribute__((always_inline)) {
+    auto B3 = [&](const char* so, auto pre, int buf, bool live) __attribute__((always_inline)) {
 #pragma unroll
         for (int s2 = 0; s2 < 32; ++s2) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+            if constexpr (SPREAD) {
+                if (s2 % P3 == P3 - 1 && DMA_B2 + s2 / P3 < 16) dma(buf, DMA_B2 + s2 / P3, live);
+            }
             if constexpr (decltype(pre)::value) {
                 if (s2 & 1) {
                     const int q = s2 >> 1;      // a0[0], b0[0..7], a0[1..7]
@@ -1661,16 +1684,19 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             barrier();
             // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); DMA of step g+2 (one per 4) ----
-            B2(buf, g + 2 < nsteps, F_{});
-            advance();
+            const bool live = g + 2 < nsteps;
+            B2(buf, live, F_{});
+            if constexpr (!SPREAD) advance();
             // K-tile g+1 landed.  Right after an epilogue (kt == 0 of a later tile) it already has:
             // the epilogue began with vmcnt(0) and B1 ended with a barrier.  Waiting here would also
             // drain every store of that epilogue (vmcnt retires loads, DMAs and stores in issue
             // order), exposing their write latency; skipped, they drain under this tile's MFMAs.
-            if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA_B2) : "memory");
             barrier();
-            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it ----
-            B3(so, pre);
+            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it (and, SPREAD,
+            // the rest of step g+2's DMAs: buf's last reader was B1, before the first barrier) ----
+            B3(so, pre, buf, live);
+            if constexpr (SPREAD) advance();
             ++g;
         };
         if constexpr (NEWLOOP) {
@@ -1756,8 +1782,11 @@ __device__ __forceinline__ float sum_lane_groups(float v) {
 //  * the next tile waits for its K-tile 0 with vmcnt(52): the 36 stores of (e) and the 16 DMAs of
 //    K-tile 1 may stay in flight.
 // Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.
-template <int ABL>      // ABL: timing ablations (bit 0 no residual loads, bit 1 no stores; wrong outputs)
+// ABL: timing ablations (bit 0 no residual loads, bit 1 no stores; wrong outputs); bit 2: a K-tile's
+// operand DMAs spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD)
+template <int ABL>
 __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
+    constexpr bool RSPREAD = (ABL & 4) != 0;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1902,7 +1931,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             const int i = (s2 >> 3) & 3, j = s2 & 7;
             if (s2 < 32) CE_MFMA_AGPR(acc[4 + i][j], b0[j], a0[4 + i]);
             else CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
-            if ((s2 & 3) == 3) {
+            if constexpr (MODE == 0 && RSPREAD) {
+                // 10 of K-tile kt + 2's DMAs here (one per 6 MFMAs), the other 6 in B3
+                if (s2 % 6 == 5 && s2 / 6 < 10) dma_k(buf, kt + 2, s2 / 6, voffA, voffW);
+            } else if ((s2 & 3) == 3) {
                 if constexpr (MODE == 0) dma_k(buf, kt + 2, s2 >> 2, voffA, voffW);
                 else dma_r(buf, MODE - 1, s2 >> 2, vr0, vr1);
             }
@@ -1919,6 +1951,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             // epilogue's 36 stores when nk == 2: 68 > 63, so the wait over-covers by 5)
             if (wait_n == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+        } else if constexpr (MODE == 0 && RSPREAD) {
+            // only this B2's 10 DMAs (+ after an epilogue its 36 stores) are younger than K-tile kt + 1
+            if (wait_n == 16) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            else if (wait_n == 52) asm volatile("s_waitcnt vmcnt(46)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             if (wait_n == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             else if (wait_n == 52) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
@@ -1929,6 +1966,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         for (int s2 = 0; s2 < 32; ++s2) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+            if constexpr (MODE == 0 && RSPREAD) {
+                // the other 6 DMAs of K-tile kt + 2 (buf's last reader was B1, before the first barrier)
+                if (s2 % 5 == 4) dma_k(buf, kt + 2, 10 + s2 / 5, voffA, voffW);
+            }
             if constexpr (MODE < 2) {
                 if (s2 & 1) {
                     const int q = s2 >> 1;
@@ -2532,7 +2573,9 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.stagger = gemm_stagger();
             plan_tail_rhl(p, nwg, w4pp_grid(nwg));
             const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
-            if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
+                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
@@ -2556,7 +2599,15 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
         const int grid = w4pp_grid(nwg);
         plan_tail_w4(p, nwg, grid);
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+            (gemm_variant() & GEMM_VAR_W4_SPREAD12))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 7>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (gemm_variant() & GEMM_VAR_W4_SPREAD8))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 11>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 3>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(grid), dim3(256), 0, s, p);
         else
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(grid), dim3(256), 0, s, p);
@@ -2625,7 +2676,15 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         p.stagger = gemm_stagger();
         const int grid = w4pp_grid(nwg);
         plan_tail_w4(p, nwg, grid);
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+            (gemm_variant() & GEMM_VAR_W4_SPREAD12))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 7>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (gemm_variant() & GEMM_VAR_W4_SPREAD8))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 11>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(grid), dim3(256), 0, s, p);
         else
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(256), 0, s, p);
