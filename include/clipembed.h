@@ -265,13 +265,16 @@ int ce_set_gemm_splitk(int enable);
  * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
 int ce_set_gemm_auto(int mode);
 /* GEMM kernel-variant bits for A/B measurement (env CE_GEMM_VARIANT at first use; a negative value
- * restores the default, bits 0|1|7): bit 0 = the four-wave persistent schedule does not drain an
+ * restores the default, bits 0|1|7|8|9): bit 0 = the four-wave persistent schedule does not drain an
  * epilogue's stores at the next tile's first K-tile; bit 1 = its epilogue written for one wave per
  * SIMD (operands staged in LDS, clipped buffer stores; also lets the default policy put GELU GEMMs on
  * that schedule); bits 2, 3, 6 = timing ablations of the LN-statistics epilogues (no residual loads /
  * no stores / no bf16 copy: wrong outputs); bit 4 = one tile per four-wave workgroup; bit 5 = split-K
  * tail on the four-wave schedule; bit 7 = the hi/lo residual GEMMs (epi 3, N % 256 == 0, grids of
- * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel.
+ * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel;
+ * bit 8 / bit 9 = the persistent four-wave / staged-residual kernel issues a K-tile's 16 operand
+ * DMAs spread over its B2 and B3 phases (10 + 6) instead of all in B2; bits 10 / 11 = a 12 + 4 /
+ * 8 + 8 split on the persistent kernel.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
 /* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key tile
