@@ -131,7 +131,9 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        GEMM_VAR_RHL_DMA_SPREAD = 512,
        // split of the spread four-wave schedule's 16 DMAs between B2 and B3: 12 + 4 or 8 + 8
        // (default 10 + 6)
-       GEMM_VAR_W4_SPREAD12 = 1024, GEMM_VAR_W4_SPREAD8 = 2048 };
+       GEMM_VAR_W4_SPREAD12 = 1024, GEMM_VAR_W4_SPREAD8 = 2048,
+       // the 10 + 6 spread with B3's DMAs in the gaps that carry no fragment read
+       GEMM_VAR_W4_SPREAD_EVEN = 4096 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD)
@@ -1646,7 +1648,13 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
             if constexpr (SPREAD) {
-                if (s2 % P3 == P3 - 1 && DMA_B2 + s2 / P3 < 16) dma(buf, DMA_B2 + s2 / P3, live);
+                if constexpr ((EV & 16) != 0 && DMA_B2 == 10) {
+                    // placed in even gaps only (the odd ones carry a set-0 fragment read)
+                    if (s2 == 4 || s2 == 10 || s2 == 14 || s2 == 20 || s2 == 24 || s2 == 30)
+                        dma(buf, DMA_B2 + (s2 - 4) / 5, live);
+                } else if (s2 % P3 == P3 - 1 && DMA_B2 + s2 / P3 < 16) {
+                    dma(buf, DMA_B2 + s2 / P3, live);
+                }
             }
             if constexpr (decltype(pre)::value) {
                 if (s2 & 1) {
@@ -2605,6 +2613,9 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
                  (gemm_variant() & GEMM_VAR_W4_SPREAD8))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 11>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (gemm_variant() & GEMM_VAR_W4_SPREAD_EVEN))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 19>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 3>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
@@ -2682,6 +2693,9 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
                  (gemm_variant() & GEMM_VAR_W4_SPREAD8))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 11>), dim3(grid), dim3(256), 0, s, p);
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (gemm_variant() & GEMM_VAR_W4_SPREAD_EVEN))
+            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 19>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))

@@ -274,7 +274,8 @@ int ce_set_gemm_auto(int mode);
  * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel;
  * bit 8 / bit 9 = the persistent four-wave / staged-residual kernel issues a K-tile's 16 operand
  * DMAs spread over its B2 and B3 phases (10 + 6) instead of all in B2; bits 10 / 11 = a 12 + 4 /
- * 8 + 8 split on the persistent kernel.
+ * 8 + 8 split on the persistent kernel; bit 12 = the 10 + 6 split with B3's DMAs in the gaps
+ * without a fragment read.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
 /* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key tile

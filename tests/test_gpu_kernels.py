@@ -100,7 +100,7 @@ def test_gemm_splitk_tail(M, N, K, variant):
 
 @pytest.mark.parametrize("M,N,K", [(33280, 1024, 1024), (20000, 3072, 1024), (17000, 1024, 4096)])
 @pytest.mark.parametrize("variant", ["gelu_bf16", "resid_f32", "bias_bf16"])
-@pytest.mark.parametrize("bits", [0, 1, 3, 35, 259, 291, 1283, 2307])
+@pytest.mark.parametrize("bits", [0, 1, 3, 35, 259, 291, 1283, 2307, 4355])
 def test_gemm_persistent_multitile(M, N, K, variant, bits):
     """The four-wave persistent schedule (SCHED 11) with several tiles per workgroup, so the
     epilogue -> next-tile hand-over (and its variant bits) runs; vs the f32 reference."""
@@ -129,7 +129,7 @@ def test_gemm_persistent_multitile(M, N, K, variant, bits):
 
 @pytest.mark.parametrize("M,N,act", [(20000, 3072, 0), (20000, 4096, 1), (20000, 4096, 2), (300, 1024, 1),
                                      (5602, 3072, 0), (4252, 4096, 1)])
-@pytest.mark.parametrize("bits", [1, 3, 35, 259, 291, 1283, 2307])
+@pytest.mark.parametrize("bits", [1, 3, 35, 259, 291, 1283, 2307, 4355])
 def test_gemm_persistent_ln_fold(M, N, act, bits):
     """SCHED 11 with the LN-fold epilogue (QKV / c_fc of the folded image tower), both epilogue
     versions (bit 1: operands staged in LDS by DMA, buffer stores clipped at row M) and the split-K
