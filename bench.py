@@ -131,7 +131,7 @@ def load_traffic(tag):
 def build_clip(args, dev, rank, world):
     import clipembed
     from clipembed import _lib, weights as W
-    from clipembed.loss import all_gather_cat
+    from clipembed.loss import ClipLoss
     cfg = clipembed.get_model_config("ViT-L-14-336")
     sd = W.synthetic_state_dict(cfg)
     model = clipembed.CLIP(cfg)
@@ -142,6 +142,10 @@ def build_clip(args, dev, rank, world):
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
     scale = float(model.logit_scale.detach().exp())
+    # the embedding exchange + local contrastive logits of open_clip's ClipLoss(local_loss=True)
+    # (loss.py:137-164): N > 1 all-gathers both embedding sets over RCCL; N = 1 is one fused
+    # logits launch both ways.  The same code runs on 2 gloo ranks in tests/test_dist_gloo.py.
+    exch = ClipLoss(local_loss=True, rank=rank, world_size=world, engine=model.engine)
 
     # the two towers are independent until the logits: the text tower runs on a second HIP stream
     # so its kernels fill the image tower's partial last rounds and launch gaps (--serial-towers:
@@ -170,14 +174,7 @@ def build_clip(args, dev, rank, world):
                 fi.record_stream(main)
             main.wait_stream(side)
             ft.record_stream(main)
-        if world > 1:
-            ai = all_gather_cat(fi, world)          # RCCL all-gather over xGMI
-            at = all_gather_cat(ft, world)
-            li, _ = model.logits(fi, at, scale, with_text_logits=False)
-            lt, _ = model.logits(ft, ai, scale, with_text_logits=False)
-        else:
-            li, lt = model.logits(fi, ft, scale)
-        return li, lt
+        return exch.get_logits(fi, ft, scale)
 
     cfgd = {"workload": "CLIP ViT-L/14-336 encode_image + encode_text + normalise + contrastive logits "
                         "(BASELINE configs[1]: batch 256/GPU bf16)",
@@ -190,8 +187,8 @@ def build_clip(args, dev, rank, world):
 
 def build_pacl(args, dev, rank, world):
     import clipembed
-    from clipembed import _lib, weights as W
-    from clipembed.loss import all_gather_cat
+    from clipembed import weights as W
+    from clipembed.loss import ClipLoss as OpenClipLoss
     from clipembed.pacl import ClipLoss, open_clip_pacl, open_clip_pacl_rope_after
     cfg = clipembed.get_model_config("ViT-L-14-336")
     sd = W.synthetic_state_dict(cfg)
@@ -203,15 +200,14 @@ def build_pacl(args, dev, rank, world):
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
     loss = ClipLoss(0.1, engine=mod.engine)        # train_pacl.py: temperature 0.1
-    labels = torch.arange(B, device=dev) + B * rank
+    # N > 1: the PACL loss over all-gathered features as open_clip's ClipLoss(local_loss=True)
+    # (loss.py:137-193; tested on 2 gloo ranks in tests/test_dist_gloo.py)
+    dist_loss = OpenClipLoss(local_loss=True, rank=rank, world_size=world, engine=mod.engine)
 
     def step():
         oi, ot = mod(imgs, caps)
         if world > 1:
-            ai, at = all_gather_cat(oi, world), all_gather_cat(ot, world)
-            li = mod.clip_model.logits(oi, at, loss.logit_scale, with_text_logits=False)[0]
-            lt = mod.clip_model.logits(ot, ai, loss.logit_scale, with_text_logits=False)[0]
-            return (loss._ce(mod.engine, li, labels) + loss._ce(mod.engine, lt, labels)) / 2
+            return dist_loss(oi, ot, loss.logit_scale)
         return loss(oi, ot)
 
     pool_flops = 2.0 * 576 * 768 * (2 if cls.weight_mode else 1)
@@ -257,8 +253,7 @@ def build_negclip(args, dev, rank, world):
 
 def build_sparc(args, dev, rank, world):
     import clipembed
-    from clipembed import _lib, weights as W
-    from clipembed.loss import all_gather_cat
+    from clipembed import weights as W
     from clipembed.pacl import SparcLoss, sparc, sparc_rope
     cfg = clipembed.get_model_config("ViT-L-14-336")
     sd = W.synthetic_state_dict(cfg)

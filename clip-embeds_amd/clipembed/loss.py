@@ -11,6 +11,8 @@ argument names and semantics (loss.py:89-193):
   * loss = (CE(logits_per_image, labels_i) + CE(logits_per_text, labels_t)) / 2.
 The exchange is torch.distributed (RCCL over xGMI with backend "nccl", gloo on CPU for tests);
 logits and cross-entropy run in libclipembed (ce_get_logits, ce_cross_entropy).  Forward only.
+bench.py's multi-GPU legs call exactly this exchange (ClipLoss.get_logits / __call__ with
+local_loss=True), and tests/test_dist_gloo.py runs it on 2 gloo ranks against the reference.
 """
 from __future__ import annotations
 
@@ -79,13 +81,19 @@ class ClipLoss:
         return self.engine
 
     def _logits(self, a: torch.Tensor, b: torch.Tensor, scale: float) -> torch.Tensor:
+        """s * a @ b^T (ce_get_logits)."""
+        return self._logits_both(a, b, scale, transpose=False)[0]
+
+    def _logits_both(self, a: torch.Tensor, b: torch.Tensor, scale: float, transpose: bool = True):
+        """(s * a @ b^T, its transpose) from one fused ce_get_logits launch (model.py:306-309)."""
         e = self._engine(a)
         a = a.float().contiguous()
         b = b.float().contiguous()
         out = torch.empty(a.shape[0], b.shape[0], device=a.device, dtype=torch.float32)
+        tout = torch.empty(b.shape[0], a.shape[0], device=a.device, dtype=torch.float32) if transpose else None
         _lib.call("ce_get_logits", e.h, _stream(e.device), _ptr(a), a.shape[0], _ptr(b), b.shape[0], a.shape[1],
-                  float(scale), 0, _ptr(out), None)
-        return out
+                  float(scale), 0, _ptr(out), _ptr(tout))
+        return out, tout
 
     def _ce(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         e = self._engine(logits)
@@ -108,9 +116,8 @@ class ClipLoss:
                 all_text = torch.cat(originals + hard, dim=0)
             if self.local_loss:
                 return self._logits(image_features, all_text, scale), self._logits(text_features, all_image, scale)
-            lpi = self._logits(all_image, all_text, scale)
-            return lpi, lpi.t().contiguous()
-        return self._logits(image_features, text_features, scale), self._logits(text_features, image_features, scale)
+            return self._logits_both(all_image, all_text, scale)
+        return self._logits_both(image_features, text_features, scale)
 
     @torch.no_grad()
     def __call__(self, image_features, text_features, logit_scale, output_dict: bool = False):

@@ -300,17 +300,84 @@ class CLIP(torch.nn.Module):
         return image_features, text_features, self.logit_scale.exp()
 
 
+PRETRAINED_DIR_ENV = "CLIPEMBED_PRETRAINED_DIR"
+
+# The pretrained tags of the registered configs (open_clip pretrained.py:308-313, _VITL14_336):
+# where open_clip would download them from, which names the local copy may carry, and the tag's
+# activation (quick_gelu), checked against the model config as factory.py:435-445 does.
+_PRETRAINED = {
+    ("ViT-L-14-336", "openai"): {
+        "hf_hub": "timm/vit_large_patch14_clip_336.openai/",
+        "url": "https://openaipublic.azureedge.net/clip/models/3035c92b350959924f9f00213499208652fc7ea050643e8b385c2dac08641f02/ViT-L-14-336px.pt",
+        "quick_gelu": True,
+    },
+}
+
+
+def list_pretrained_tags_by_model(model_name: str):
+    """open_clip pretrained.list_pretrained_tags_by_model for the registered configs."""
+    return [t for (m, t) in _PRETRAINED if m == model_name]
+
+
+def pretrained_candidates(model_name: str, tag: str, root: str):
+    """Local file names searched under $CLIPEMBED_PRETRAINED_DIR for (model, tag), in order: the
+    Hugging Face hub layout open_clip downloads (`<repo basename>/open_clip_model.safetensors`, then
+    `open_clip_pytorch_model.bin`: HF_SAFE_WEIGHTS_NAME / HF_WEIGHTS_NAME, constants.py:9-10,
+    preferred in that order by pretrained.py:784-797), the same two names under `<model>/<tag>/`,
+    a flat `<model>-<tag>.{safetensors,bin,pt}`, and the URL's file name (`ViT-L-14-336px.pt`)."""
+    import os
+    cfg = _PRETRAINED[(model_name, tag)]
+    hub = cfg["hf_hub"].strip("/").split("/")[-1]
+    names = []
+    for d in (hub, os.path.join(model_name, tag)):
+        names += [os.path.join(d, "open_clip_model.safetensors"), os.path.join(d, "open_clip_pytorch_model.bin")]
+    names += [f"{model_name}-{tag}.{ext}" for ext in ("safetensors", "bin", "pt")]
+    names.append(os.path.basename(cfg["url"]))
+    return [os.path.join(root, n) for n in names]
+
+
+def resolve_pretrained(model_name: str, pretrained: str, quick_gelu: bool = False) -> str:
+    """The checkpoint file for `pretrained` (factory.py:390-419): an existing file path is used as
+    is; a known tag (pretrained.py:308-313) resolves to a local copy under $CLIPEMBED_PRETRAINED_DIR
+    (there is no download: the engine never touches the network), with a RuntimeError naming the
+    variable when it is unset or holds no copy; anything else raises the reference's error."""
+    import os
+    import warnings
+    if os.path.isfile(pretrained):
+        return pretrained
+    tag = pretrained.lower()
+    if (model_name, tag) not in _PRETRAINED:
+        raise RuntimeError(f"Pretrained value '{pretrained}' is not a known tag or valid file path "
+                           f"(known tags for {model_name}: {list_pretrained_tags_by_model(model_name)})")
+    root = os.environ.get(PRETRAINED_DIR_ENV)
+    if not root:
+        raise RuntimeError(f"pretrained='{pretrained}' for {model_name} needs a local copy of the weights: set "
+                           f"{PRETRAINED_DIR_ENV} to the directory holding it (open_clip would download "
+                           f"{_PRETRAINED[(model_name, tag)]['hf_hub']}; clipembed never downloads)")
+    cands = pretrained_candidates(model_name, tag, root)
+    for c in cands:
+        if os.path.isfile(c):
+            if _PRETRAINED[(model_name, tag)]["quick_gelu"] != quick_gelu:
+                warnings.warn(f"QuickGELU mismatch between final model config (quick_gelu={quick_gelu}) and "
+                              f"pretrained tag '{pretrained}' (quick_gelu={_PRETRAINED[(model_name, tag)]['quick_gelu']}).",
+                              UserWarning)
+            return c
+    raise RuntimeError(f"pretrained='{pretrained}' for {model_name}: no checkpoint under {PRETRAINED_DIR_ENV}={root}; "
+                       f"looked for {cands}")
+
+
 def create_model(model_name: str = "ViT-L-14-336", pretrained: Optional[str] = None, device=None,
                  state_dict: Optional[dict] = None, output_dict: bool = False, **_ignored) -> CLIP:
     """open_clip.create_model equivalent (factory.py:241-613) for the registered CLIP configs.
 
-    pretrained: None (weights must then be supplied via `state_dict`/load_state_dict) or a path
-    to a local open_clip state dict (.pt/.bin loaded with weights_only=True, or .safetensors).
+    pretrained: None (weights must then be supplied via `state_dict`/load_state_dict), a path to a
+    local open_clip state dict (.pt/.bin loaded with weights_only=True, or .safetensors), or a known
+    tag ('openai'), resolved to a local file by resolve_pretrained ($CLIPEMBED_PRETRAINED_DIR).
     """
     cfg = get_model_config(model_name)
     model = CLIP(cfg, output_dict=output_dict)
     if pretrained:
-        load_checkpoint(model, pretrained)
+        load_checkpoint(model, resolve_pretrained(model_name, pretrained, cfg.quick_gelu))
     if state_dict is not None:
         model.load_state_dict(state_dict)
     if device is not None:

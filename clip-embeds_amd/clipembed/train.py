@@ -11,7 +11,8 @@ open_clip/src/train-clip.sh (`--lock-image --local-loss --gather-with-grad [--us
      (:144-153), local-loss logits [B, sum T] and [T_local, W*B], labels arange + B*rank with -100
      for hard negatives (:127-135), loss = (CE_i + CE_t) / 2;
   4. backward of the loss to the features (ce_contrastive_grad); the all-gather's backward (sum of
-     every rank's gradient of this rank's rows) is an RCCL all_reduce of d(all text features);
+     every rank's gradient of this rank's rows) is an RCCL reduce_scatter of d(all text features),
+     laid out in the gather's padded per-rank chunks;
   5. text-tower backward into one flat f32 gradient buffer (ce_text_backward), DDP's gradient
      all-reduce as ONE RCCL all_reduce(AVG) of that buffer (main.py:302);
   6. AdamW on the flat f32 masters, two groups as main.py:335-349 (gain/bias/ln/logit_scale
@@ -189,6 +190,10 @@ class TextTowerTrainer:
         """Steps 1-5: forward, ClipLoss, backward, gradient all-reduce.  Returns the local loss (device
         scalar, no host sync); gradients are in self.grad / self.gviews."""
         img = self.model.encode_image(images, normalize=True)
+        return self.compute_grads_from_features(img, texts)
+
+    def compute_grads_from_features(self, img: torch.Tensor, texts: torch.Tensor) -> torch.Tensor:
+        """Steps 2-5 given the locked image tower's normalised features img [B, E] (step 1)."""
         txt = self.text_forward(texts)
         scale = math.exp(float(self.logit_scale))
         dtxt = self.loss_and_feature_grad(img, txt, scale)

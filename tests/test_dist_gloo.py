@@ -29,8 +29,9 @@ def _worker(rank, world, port, q):
     from oracle import clip_oracle as O
 
     class CpuCheckedLoss(ClipLoss):     # test double: oracle arithmetic, product exchange logic
-        def _logits(self, a, b, scale):
-            return torch.from_numpy(np.float32(scale) * a.numpy() @ b.numpy().T)
+        def _logits_both(self, a, b, scale, transpose=True):
+            z = torch.from_numpy(np.float32(scale) * a.numpy() @ b.numpy().T)
+            return z, (z.t().contiguous() if transpose else None)
 
         def _ce(self, logits, labels):
             return torch.tensor(O.cross_entropy(logits.numpy(), labels.numpy()))
@@ -40,7 +41,11 @@ def _worker(rank, world, port, q):
     B, D, K = 4, 768, [2, 3][rank]
     img = torch.from_numpy(O.l2normalize(W.uniform(f"neg-img-{rank}", B * D).reshape(B, D)))
     txt = torch.from_numpy(O.l2normalize(W.uniform(f"neg-txt-{rank}", (B + K) * D).reshape(B + K, D)))
+    # the bench's exchange (bench.py build_clip / build_pacl): ClipLoss(local_loss=True).get_logits
+    exch = CpuCheckedLoss(local_loss=True, rank=rank, world_size=world)
+    li, lt = exch.get_logits(img, txt[:B], 14.2857)
     res = {
+        "bench_li": li.numpy(), "bench_lt": lt.numpy(), "img": img.numpy(), "txt": txt[:B].numpy(),
         "hard": float(CpuCheckedLoss(local_loss=True, rank=rank, world_size=world, usehardtext=True)(img, txt, 14.2857)),
         "plain_local": float(CpuCheckedLoss(local_loss=True, rank=rank, world_size=world)(img, txt[:B], 14.2857)),
         "plain_global": float(CpuCheckedLoss(local_loss=False, rank=rank, world_size=world)(img, txt[:B], 14.2857)),
@@ -62,9 +67,22 @@ def test_negclip_exchange_two_ranks(golden):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    all_img = np.concatenate([got[r]["img"] for r in range(2)])
+    all_txt = np.concatenate([got[r]["txt"] for r in range(2)])
     for r in range(2):
         for k in ("hard", "plain_local", "plain_global"):
             np.testing.assert_allclose(got[r][k], float(g[f"{k}_r{r}"]), rtol=1e-5, err_msg=f"{k} rank {r}")
+        # bench.py's exchange: this rank's rows against every rank's embeddings, rank order
+        # (loss.py:155-157: logits_per_image = s I_local T_all^T, logits_per_text = s T_local I_all^T)
+        li, lt = got[r]["bench_li"], got[r]["bench_lt"]
+        assert li.shape == (4, 8) and lt.shape == (4, 8)
+        np.testing.assert_allclose(li, np.float32(14.2857) * got[r]["img"] @ all_txt.T, rtol=1e-6)
+        np.testing.assert_allclose(lt, np.float32(14.2857) * got[r]["txt"] @ all_img.T, rtol=1e-6)
+        # and its loss is the reference's 2-rank ClipLoss(local_loss=True)
+        lab = np.arange(4) + 4 * r
+        from oracle import clip_oracle as O
+        loss = (O.cross_entropy(li, lab) + O.cross_entropy(lt, lab)) / 2
+        np.testing.assert_allclose(loss, float(g[f"plain_local_r{r}"]), rtol=1e-5)
 
 
 def _train_worker(rank, world, port, q):

@@ -1,0 +1,138 @@
+"""The NegCLIP text-tower step at the C4 per-GPU workload (BASELINE configs[3]; exactly what
+`bench.py --workload negclip` times): full-depth ViT-L-14-336, 1,024 images + 512 hard-negative
+captions per GPU, so the text tower runs M = 1,536 x 77 = 118,272 rows through 12 blocks.
+
+At that size the GEMM policy picks paths the toy-size test (tests/test_gpu_train.py, M = 462)
+never reaches: the four-wave persistent kernel for the forward QKV / c_fc GEMMs and every dX GEMM,
+and split-K + fixup for every weight-gradient GEMM (dW_*: grids of 9-36 tiles with K = 118,272).
+The test asserts those paths fired (ce_gemm_path_counts) and checks the step against
+  * the same step on the plain path (ce_set_gemm_auto(0) + ce_set_gemm_splitk(0): the 4-phase
+    kernel only, no split-K): loss and every gradient tensor, cosine >= 0.9999;
+  * the reference's f32 autograd of the same step (oracle/text_train_torch.py, pinned to the
+    reference's own training step in tests/test_oracle_train.py), run here in f32 on the GPU:
+    every gradient tensor cosine >= 0.995 and norm within 3 %, loss within 5e-3 (the engine's
+    GEMMs are bf16 with f32 accumulation, standing in for the reference's --precision amp).
+Reference: open_clip_train/train.py:85-112, open_clip/src/open_clip/loss.py:67-193."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import clipembed
+from clipembed import _lib, weights as W
+from clipembed.config import get_model_config
+from clipembed.train import TextTowerTrainer
+
+pytestmark = pytest.mark.gpu
+
+B_IMG, K_HARD = 1024, 512
+# ce_gemm_path_counts indices (include/clipembed.h): path + epilogue (0 = plain)
+W4PP, NT, FIXUP = 0, 3, 6
+
+
+def path_counts(reset=True):
+    c = (ctypes.c_int64 * 13)()
+    _lib.call("ce_gemm_path_counts", c, 13, 1 if reset else 0)
+    return list(c)
+
+
+def _cos(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def c4():
+    cfg = get_model_config("ViT-L-14-336")
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(W.synthetic_state_dict(cfg))
+    m.to("cuda")
+    tr = TextTowerTrainer(m, lr=5e-6, usehardtext=True)
+    imgs = torch.from_numpy(W.synthetic_images(B_IMG, seed=1000)).cuda()
+    caps = torch.from_numpy(W.synthetic_captions(B_IMG + K_HARD, seed=2000)).cuda()
+    img = m.encode_image(imgs, normalize=True)
+    del imgs
+    torch.cuda.synchronize()
+
+    def run():
+        tr.grad.fill_(float("nan"))           # every gradient slot must be written by the step
+        loss = float(tr.compute_grads_from_features(img, caps))
+        torch.cuda.synchronize()
+        return loss, tr.grad.clone()
+
+    path_counts()
+    loss_big, g_big = run()
+    cnt_big = path_counts()
+    L = _lib.lib()
+    pa, ps = L.ce_set_gemm_auto(0), L.ce_set_gemm_splitk(0)
+    try:
+        path_counts()
+        loss_plain, g_plain = run()
+        cnt_plain = path_counts()
+    finally:
+        L.ce_set_gemm_auto(pa)
+        L.ce_set_gemm_splitk(ps)
+    return dict(m=m, tr=tr, img=img, caps=caps, loss_big=loss_big, g_big=g_big, cnt_big=cnt_big,
+                loss_plain=loss_plain, g_plain=g_plain, cnt_plain=cnt_plain)
+
+
+def _views(tr, flat):
+    out = {}
+    for n, v in tr.gviews.items():
+        off = (v.data_ptr() - tr.grad.data_ptr()) // 4
+        out[n] = flat[off:off + v.numel()].view(v.shape)
+    out["logit_scale"] = flat[-1:]
+    return out
+
+
+def test_big_grid_paths_fire(c4):
+    """Per text block: QKV, c_fc and the four dX GEMMs on the four-wave persistent kernel; the four
+    dW GEMMs on the 4-phase kernel with split-K + fixup; out-proj / c_proj (residual epilogue) on
+    the 4-phase kernel.  The plain run uses neither the persistent kernel nor split-K."""
+    nl = 12
+    cnt = c4["cnt_big"]
+    assert cnt[W4PP] == 6 * nl, cnt
+    assert cnt[FIXUP] == 4 * nl, cnt
+    assert cnt[NT] == 6 * nl, cnt
+    assert sum(cnt) == 16 * nl, cnt
+    cp = c4["cnt_plain"]
+    assert cp[W4PP] == 0 and cp[FIXUP] == 0 and cp[NT] == 16 * nl and sum(cp) == 16 * nl, cp
+
+
+def test_gradients_finite_and_paths_agree(c4):
+    """Big-grid paths vs the plain path: the same step up to f32 summation order (and the bf16
+    rounding of intermediate gradients that order can flip)."""
+    assert math.isfinite(c4["loss_big"])
+    assert abs(c4["loss_big"] - c4["loss_plain"]) <= 1e-4 * abs(c4["loss_plain"])
+    assert torch.isfinite(c4["g_big"]).all() and torch.isfinite(c4["g_plain"]).all()
+    vb, vp = _views(c4["tr"], c4["g_big"]), _views(c4["tr"], c4["g_plain"])
+    bad = []
+    for n in vb:
+        if vp[n].abs().max() == 0:
+            assert vb[n].abs().max() == 0, n
+            continue
+        c = _cos(vb[n], vp[n])
+        if c < 0.9999:
+            bad.append((n, round(c, 6)))
+    assert not bad, bad
+
+
+def test_matches_f32_autograd_restatement(c4):
+    """The engine's gradients at the C4 size vs the reference's f32 autograd of the same step."""
+    from oracle.text_train_torch import TorchTextTrainStep
+    m, tr = c4["m"], c4["tr"]
+    ref_step = TorchTextTrainStep(m._sd, m.cfg, device="cuda")
+    loss_ref, g_ref = ref_step.loss_and_grads(c4["img"], c4["caps"], float(tr.logit_scale))
+    del ref_step
+    np.testing.assert_allclose(c4["loss_big"], loss_ref, rtol=5e-3)
+    ours = _views(tr, c4["g_big"])
+    bad = []
+    for n, r in g_ref.items():
+        o = ours[n].reshape(r.shape)
+        c = _cos(o, r)
+        nr = float(o.double().norm() / (r.double().norm() + 1e-30))
+        if not (c >= 0.995 and abs(nr - 1) < 0.03):
+            bad.append((n, round(c, 5), round(nr, 4)))
+    assert not bad, bad

@@ -100,3 +100,43 @@ def test_pacl_checkpoint_layout(small_sd):
     mod.load_state_dict(ckpt)
     _same(mod.clip_model, sd)
     assert set(mod._heads) == set(heads) and all(torch.equal(mod._heads[k], heads[k]) for k in heads)
+
+
+def test_pretrained_tag_needs_local_dir(monkeypatch):
+    """eval_clip.py:21 passes pretrained='openai': the tag (pretrained.py:308-313) resolves to a
+    local copy under $CLIPEMBED_PRETRAINED_DIR; unset, the error names the variable."""
+    from clipembed.model import PRETRAINED_DIR_ENV, resolve_pretrained
+    monkeypatch.delenv(PRETRAINED_DIR_ENV, raising=False)
+    with pytest.raises(RuntimeError, match=PRETRAINED_DIR_ENV):
+        clipembed.create_model("ViT-L-14-336", pretrained="openai")
+    with pytest.raises(RuntimeError, match="not a known tag or valid file path"):
+        resolve_pretrained("ViT-L-14-336", "laion2b_nonexistent")
+
+
+@pytest.mark.parametrize("layout", ["vit_large_patch14_clip_336.openai/open_clip_model.safetensors",
+                                    "vit_large_patch14_clip_336.openai/open_clip_pytorch_model.bin",
+                                    "ViT-L-14-336/openai/open_clip_model.safetensors",
+                                    "ViT-L-14-336-openai.safetensors"])
+def test_pretrained_tag_resolves_local_copy(tmp_path, monkeypatch, layout):
+    """create_model('ViT-L-14-336', pretrained='openai') loads the local copy through
+    load_checkpoint (factory.py:390-404 + 171-215); the tag's quick_gelu=True against the GELU
+    config warns as factory.py:435-445 does."""
+    from clipembed.model import PRETRAINED_DIR_ENV, resolve_pretrained
+    path = tmp_path / layout
+    path.parent.mkdir(parents=True, exist_ok=True)
+    sd = {"logit_scale": torch.tensor([math.log(100.0)]), "ln_final.weight": torch.arange(768, dtype=torch.float32)}
+    if layout.endswith(".safetensors"):
+        from safetensors.torch import save_file
+        save_file(sd, str(path))
+    else:
+        torch.save(sd, path)
+    monkeypatch.setenv(PRETRAINED_DIR_ENV, str(tmp_path))
+    assert resolve_pretrained("ViT-L-14-336", "openai", quick_gelu=True) == str(path)
+    with pytest.warns(UserWarning, match="QuickGELU mismatch"):
+        m = clipembed.create_model("ViT-L-14-336", pretrained="openai")
+    assert float(m.logit_scale.detach()) == pytest.approx(math.log(100.0))
+    assert torch.equal(m.state_dict()["ln_final.weight"], sd["ln_final.weight"])
+    (tmp_path / "empty").mkdir()
+    monkeypatch.setenv(PRETRAINED_DIR_ENV, str(tmp_path / "empty"))
+    with pytest.raises(RuntimeError, match="no checkpoint under"):
+        resolve_pretrained("ViT-L-14-336", "openai")
