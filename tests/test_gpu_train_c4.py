@@ -98,7 +98,7 @@ def test_big_grid_paths_fire(c4):
     assert cnt[NT] == 6 * nl, cnt
     assert sum(cnt) == 16 * nl, cnt
     cp = c4["cnt_plain"]
-    assert cp[W4PP] == 0 and cp[FIXUP] == 0 and cp[NT] == 16 * nl and sum(cp) == 16 * nl, cp
+    assert cp[W4PP] == 0 and cp[FIXUP] == 0 and cp[NT] == 12 * nl and sum(cp) == 12 * nl, cp
 
 
 def test_gradients_finite_and_paths_agree(c4):

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One parameterised GPU-box pass.  Usage: tools/gpu_run.sh TAG STEP...  where STEP is one of
+#   tests:<pytest args, comma-separated>   verbose pytest on the given files / -k filters
+#   gputests                               the whole -m gpu suite
+#   smoke                                  __graft_entry__.smoke()
+#   bench:<bench.py args, comma-separated> one bench.py run (JSON line -> gpurun_out/TAG_benchN.log)
+#   rocprof:<bench.py args>                rocprofv3 --kernel-trace --stats of one bench.py run
+# Every step has its own time limit; the chain stops at the first failure.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+TAG=$1; shift
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
+  args=${arg//,/ }
+  case $kind in
+    tests)   timeout -k 10 900 python -u -m pytest $args -v --timeout 300 --timeout-method thread \
+               > gpurun_out/${TAG}_tests$n.log 2>&1 ;;
+    gputests) timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+               > gpurun_out/${TAG}_gputests.log 2>&1 ;;
+    smoke)   timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1 ;;
+    bench)   timeout -k 10 400 python -u bench.py $args > gpurun_out/${TAG}_bench$n.log 2>&1 ;;
+    rocprof) timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$n -o run -- \
+               python3 -u bench.py --no-cpu-baseline $args > gpurun_out/${TAG}_prof$n.log 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $n $step: rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
