@@ -138,6 +138,8 @@ struct ce_handle {
     size_t ws_t_bytes = 0;   // concurrently with encode_image
     char* tmp = nullptr;
     size_t tmp_bytes = 0;
+    char* pool = nullptr;        // PACL pooling: per-split partial rows
+    size_t pool_bytes = 0;
     float* scratch = nullptr;    // 256 B
     // device preprocessing: tap tables (pinned host staging -> device), intermediate rows
     char* prep_host = nullptr;
@@ -985,6 +987,7 @@ int ce_destroy(ce_handle* h) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->ws_t) (void)hipFree(h->ws_t);
     if (h->tmp) (void)hipFree(h->tmp);
+    if (h->pool) (void)hipFree(h->pool);
     if (h->tr) (void)hipFree(h->tr);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->prep_host) (void)hipHostFree(h->prep_host);
@@ -1354,10 +1357,11 @@ int ce_pacl_pool(ce_handle* h, void* stream, const void* visual_proj, int vp_dty
         else return fail(CE_ERR_INVALID, "ce_pacl_pool: no RoPE table for P=%d D=%d", P, Dp);
     }
     const int R = Bi > Bt ? Bi : Bt;
+    CE_TRY(grow_buffer(h->pool, h->pool_bytes, ce::pacl_pool_part_bytes(R, P, Dp)));
     return timed(h, s, "pacl_pool", 2.0 * R * P * Dp * (weight_mode ? 2 : 1),
                  (double)Bi * P * Dp * (vp_dtype == CE_BF16 ? 2 : 4) + 4.0 * Bt * Dp + 4.0 * R * Dp,
                  [&] { return ce::launch_pacl_pool(visual_proj, vp_dtype == CE_BF16, Bi, P, text_proj, Bt, Dp,
-                                                   weight_mode, rc, rs, out_img, out_txt, s); });
+                                                   weight_mode, rc, rs, out_img, out_txt, (float*)h->pool, s); });
 }
 
 int ce_pacl_forward(ce_handle* h, void* stream, const void* pixels, int pixel_dtype, int Bi, const int64_t* ids,

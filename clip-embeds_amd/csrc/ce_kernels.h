@@ -133,9 +133,11 @@ hipError_t launch_l2norm(float* out, const float* x, int rows, int D, hipStream_
 hipError_t launch_cross_entropy_rows(float* accum, const float* logits, int R, int C,
                                      const int64_t* labels, hipStream_t s);
 hipError_t launch_cross_entropy_finish(float* loss, const float* accum, hipStream_t s);
+// part: f32 scratch of pacl_pool_part_bytes(max(Bi, Bt), P, D) bytes (per-split partial rows)
 hipError_t launch_pacl_pool(const void* vp, bool vp_bf16, int Bi, int P, const float* tp, int Bt,
                             int D, int weight_mode, const float* rope_cos, const float* rope_sin,
-                            float* out_img, float* out_txt, hipStream_t s);
+                            float* out_img, float* out_txt, float* part, hipStream_t s);
+size_t pacl_pool_part_bytes(int R, int P, int D);
 // SPARC row step in place on sim [rows][P]: min-max normalise, zero below sigma, divide by sum
 hipError_t launch_sparc_weights(float* sim, long rows, int P, float sigma, hipStream_t s);
 hipError_t launch_rope(float* out, const float* x, int B, int P, int D, const float* cos_t,

@@ -79,107 +79,197 @@ __global__ __launch_bounds__(256) void fgemm_k(FGemmParams p) {
 }
 
 // ---- fused PACL pooling -----------------------------------------------------------------
-// One 256-thread block per output row; D <= 1024, D % 128 == 0 (768 for ViT-L-14-336).
+// Two passes.  Pass 1 (pacl_pool_part_k): grid = R output rows x S patch splits; each 256-thread
+// workgroup streams its P/S patches of one image, one patch row per wave at a time, every lane
+// loading 16-B chunks (8 bf16) of the row (chunk q = c * 64 + lane, elements 8q .. 8q + 7, valid
+// while 8q < D), two patches in flight per wave; MODE 1 forms the wave's dot(t_n, v_p) and |v_p|^2
+// (after RoPE for ROPE) with two wave reductions and w_p = sigmoid(10 cos); the four waves' sums
+// meet in LDS and leave as one f32 partial row part[row][split][D].  Pass 2 (pacl_pool_finish_k):
+// per output row the S partials in a fixed order, L2-normalised; the normalised text rows.
+// D <= 1024, D % 128 == 0 (768 for ViT-L-14-336).
+constexpr int PP_NC = 2;           // 16-B chunks per lane per patch row (D <= 1024 bf16)
+
+template <bool VP_BF16>
+__device__ __forceinline__ void pp_load(const void* vp, size_t rbase, int q, float (&x)[8]) {
+    if constexpr (VP_BF16) {
+        const uint4 u = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(vp) + rbase + 8 * q);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[2 * k] = __uint_as_float(w[k] << 16);
+            x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        }
+    } else {
+        const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(vp) + rbase + 8 * q);
+        const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(vp) + rbase + 8 * q + 4);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    }
+}
+
 template <bool VP_BF16, int MODE, bool ROPE>
-__global__ __launch_bounds__(256) void pacl_pool_k(const void* __restrict__ vp, int Bi, int P,
-                                                   const float* __restrict__ tp, int Bt, int D,
-                                                   const float* __restrict__ rc,
-                                                   const float* __restrict__ rs,
-                                                   float* __restrict__ out_img,
-                                                   float* __restrict__ out_txt) {
-    __shared__ float tn[1024];
-    __shared__ float part[4][1024];
-    __shared__ float red[4];
-    const int row = blockIdx.x;
+__global__ __launch_bounds__(256) void pacl_pool_part_k(const void* __restrict__ vp, int Bi, int P,
+                                                        const float* __restrict__ tp, int Bt, int D,
+                                                        const float* __restrict__ rc,
+                                                        const float* __restrict__ rs, int S,
+                                                        float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float tn[1024];
+    __shared__ __attribute__((aligned(16))) float red[4][1024];
+    const int row = blockIdx.x / S, split = blockIdx.x - row * S;
     const int img = Bi == 1 ? 0 : row;
     const int txt = Bt == 1 ? 0 : row;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-    // normalised text vector
-    float ss = 0.f;
-    for (int d = tid; d < D; d += 256) { const float t = tp[(size_t)txt * D + d]; tn[d] = t; ss += t * t; }
-    ss = wave_sum(ss);
-    if (lane == 0) red[wave] = ss;
-    __syncthreads();
-    const float tinv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
-    for (int d = tid; d < D; d += 256) tn[d] *= tinv;
-    __syncthreads();
-    if (row < Bt && out_txt)
-        for (int d = tid; d < D; d += 256) out_txt[(size_t)row * D + d] = tn[d];
-
-    // each lane owns NE = D/64 consecutive-pair elements: e = 2*(c*64 + lane) + {0,1}
-    constexpr int MAXC = 8;    // D <= 1024
-    const int NCH = D / 128;
-    float acc[MAXC][2];
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) { acc[c][0] = 0.f; acc[c][1] = 0.f; }
     const int half = D / 2;
-    for (int p = wave; p < P; p += 4) {
-        const size_t rbase = ((size_t)img * P + p) * D;
-        float x[MAXC][2];
+    if constexpr (MODE == 1) {
+        // normalised text vector (F.normalize, pacl.py:123)
+        float ss = 0.f;
+        for (int d = tid; d < D; d += 256) { const float t = tp[(size_t)txt * D + d]; tn[d] = t; ss = fmaf(t, t, ss); }
+        ss = wave_sum(ss);
+        if (lane == 0) red[0][wave] = ss;
+        __syncthreads();
+        const float tinv = 1.0f / fmaxf(sqrtf((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])), 1e-12f);
+        for (int d = tid; d < D; d += 256) tn[d] *= tinv;
+        __syncthreads();
+    }
+    const int p0 = (int)((long)split * P / S), p1 = (int)((long)(split + 1) * P / S);
+    float acc[PP_NC][8];
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) {
-            if (c < NCH) {
-                const int e = 2 * (c * 64 + lane);
-                if constexpr (VP_BF16) {
-                    const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const bf16_t*>(vp) + rbase + e);
-                    x[c][0] = bf2f((bf16_t)(u & 0xffff));
-                    x[c][1] = bf2f((bf16_t)(u >> 16));
-                } else {
-                    const float2 f = *reinterpret_cast<const float2*>(static_cast<const float*>(vp) + rbase + e);
-                    x[c][0] = f.x; x[c][1] = f.y;
-                }
-            }
-        }
-        float w = 1.0f;
-        if constexpr (MODE == 1) {
+    for (int c = 0; c < PP_NC; ++c)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
+    // weight of one patch row (MODE 1): sigmoid(10 cos(t_n, [rope](v_p)))  (pacl.py:120-127,199-209)
+    auto weight = [&](int p, const float (&x)[PP_NC][8]) -> float {
+        if constexpr (MODE == 0) {
+            return 1.0f;
+        } else {
             float dot = 0.f, nrm = 0.f;
 #pragma unroll
-            for (int c = 0; c < MAXC; ++c) {
-                if (c < NCH) {
-                    const int e = 2 * (c * 64 + lane);
+            for (int c = 0; c < PP_NC; ++c) {
+                const int q = c * 64 + lane;
+                if (8 * q < D) {
                     if constexpr (ROPE) {
-                        const int i = e / 2;   // pair index
-                        const float cs = rc[(size_t)p * half + i], sn = rs[(size_t)p * half + i];
-                        const float lo = x[c][0] * cs - x[c][1] * sn;
-                        const float hi = x[c][0] * sn + x[c][1] * cs;
-                        dot += lo * tn[i] + hi * tn[half + i];
-                        nrm += lo * lo + hi * hi;
+                        // pairs (8q + 2k, 8q + 2k + 1) -> positions i = 4q + k and half + i (Q7)
+                        const float4 cs = *reinterpret_cast<const float4*>(rc + (size_t)p * half + 4 * q);
+                        const float4 sn = *reinterpret_cast<const float4*>(rs + (size_t)p * half + 4 * q);
+                        const float4 tl = *reinterpret_cast<const float4*>(tn + 4 * q);
+                        const float4 th = *reinterpret_cast<const float4*>(tn + half + 4 * q);
+                        const float c4[4] = {cs.x, cs.y, cs.z, cs.w}, s4[4] = {sn.x, sn.y, sn.z, sn.w};
+                        const float l4[4] = {tl.x, tl.y, tl.z, tl.w}, h4[4] = {th.x, th.y, th.z, th.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const float lo = x[c][2 * k] * c4[k] - x[c][2 * k + 1] * s4[k];
+                            const float hi = x[c][2 * k] * s4[k] + x[c][2 * k + 1] * c4[k];
+                            dot += lo * l4[k] + hi * h4[k];
+                            nrm += lo * lo + hi * hi;
+                        }
                     } else {
-                        dot += x[c][0] * tn[e] + x[c][1] * tn[e + 1];
-                        nrm += x[c][0] * x[c][0] + x[c][1] * x[c][1];
+                        const float4 ta = *reinterpret_cast<const float4*>(tn + 8 * q);
+                        const float4 tb = *reinterpret_cast<const float4*>(tn + 8 * q + 4);
+                        const float t8[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            dot = fmaf(x[c][k], t8[k], dot);
+                            nrm = fmaf(x[c][k], x[c][k], nrm);
+                        }
                     }
                 }
             }
             dot = wave_sum(dot);
             nrm = wave_sum(nrm);
             const float cosv = dot / fmaxf(sqrtf(nrm), 1e-12f);
-            w = 1.0f / (1.0f + expf(-10.0f * cosv));
+            return 1.0f / (1.0f + expf(-10.0f * cosv));
         }
+    };
+    auto load_row = [&](int p, float (&x)[PP_NC][8]) {
+        const size_t rbase = ((size_t)img * P + p) * D;
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c)
-            if (c < NCH) { acc[c][0] = fmaf(w, x[c][0], acc[c][0]); acc[c][1] = fmaf(w, x[c][1], acc[c][1]); }
+        for (int c = 0; c < PP_NC; ++c) {
+            const int q = c * 64 + lane;
+            if (8 * q < D) pp_load<VP_BF16>(vp, rbase, q, x[c]);
+            else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[c][k] = 0.f;
+            }
+        }
+    };
+    int p = p0 + wave;
+    // two patch rows in flight per wave
+    for (; p + 4 < p1; p += 8) {
+        float xa[PP_NC][8], xb[PP_NC][8];
+        load_row(p, xa);
+        load_row(p + 4, xb);
+        const float wa = weight(p, xa), wb = weight(p + 4, xb);
+#pragma unroll
+        for (int c = 0; c < PP_NC; ++c)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[c][k] = fmaf(wb, xb[c][k], fmaf(wa, xa[c][k], acc[c][k]));
     }
+    if (p < p1) {
+        float xa[PP_NC][8];
+        load_row(p, xa);
+        const float wa = weight(p, xa);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-        if (c < NCH) {
-            const int e = 2 * (c * 64 + lane);
-            part[wave][e] = acc[c][0];
-            part[wave][e + 1] = acc[c][1];
+        for (int c = 0; c < PP_NC; ++c)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[c][k] = fmaf(wa, xa[c][k], acc[c][k]);
+    }
+    // the four waves' sums, fixed order, one partial row
+#pragma unroll
+    for (int c = 0; c < PP_NC; ++c) {
+        const int q = c * 64 + lane;
+        if (8 * q < D) {
+            *reinterpret_cast<float4*>(&red[wave][8 * q]) = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+            *reinterpret_cast<float4*>(&red[wave][8 * q + 4]) = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
         }
+    }
     __syncthreads();
-    float s2 = 0.f;
-    for (int d = tid; d < D; d += 256) {
-        const float v = (part[0][d] + part[1][d]) + (part[2][d] + part[3][d]);
-        part[0][d] = v;
-        s2 += v * v;
+    float* dst = part + (size_t)blockIdx.x * D;
+    for (int d4 = tid; d4 < D / 4; d4 += 256) {
+        const float4 a = *reinterpret_cast<const float4*>(&red[0][4 * d4]);
+        const float4 b = *reinterpret_cast<const float4*>(&red[1][4 * d4]);
+        const float4 c = *reinterpret_cast<const float4*>(&red[2][4 * d4]);
+        const float4 e = *reinterpret_cast<const float4*>(&red[3][4 * d4]);
+        *reinterpret_cast<float4*>(dst + 4 * d4) =
+            make_float4((a.x + b.x) + (c.x + e.x), (a.y + b.y) + (c.y + e.y), (a.z + b.z) + (c.z + e.z),
+                        (a.w + b.w) + (c.w + e.w));
+    }
+}
+
+// Pass 2: out_img[row] = normalize(sum_split part[row][split]); out_txt[row] = normalize(tp[row])
+__global__ __launch_bounds__(256) void pacl_pool_finish_k(const float* __restrict__ part, int S, int D,
+                                                          const float* __restrict__ tp, int Bt,
+                                                          float* __restrict__ out_img,
+                                                          float* __restrict__ out_txt) {
+    __shared__ float red[2][4];
+    const int row = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};     // D <= 1024: elements tid + 256 k
+    float s2 = 0.f, st = 0.f;
+    const float* pr = part + (size_t)row * S * D;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int d = tid + 256 * k;
+        if (d < D) {
+            float a = 0.f;
+            for (int sp = 0; sp < S; ++sp) a += pr[(size_t)sp * D + d];
+            v[k] = a;
+            s2 = fmaf(a, a, s2);
+            if (out_txt && row < Bt) { const float t = tp[(size_t)row * D + d]; st = fmaf(t, t, st); }
+        }
     }
     s2 = wave_sum(s2);
+    st = wave_sum(st);
+    if (lane == 0) { red[0][wave] = s2; red[1][wave] = st; }
     __syncthreads();
-    if (lane == 0) red[wave] = s2;
-    __syncthreads();
-    const float inv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
-    for (int d = tid; d < D; d += 256) out_img[(size_t)row * D + d] = part[0][d] * inv;
+    const float inv = 1.0f / fmaxf(sqrtf((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])), 1e-12f);
+    const float tinv = 1.0f / fmaxf(sqrtf((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])), 1e-12f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int d = tid + 256 * k;
+        if (d < D) {
+            out_img[(size_t)row * D + d] = v[k] * inv;
+            if (out_txt && row < Bt) out_txt[(size_t)row * D + d] = tp[(size_t)row * D + d] * tinv;
+        }
+    }
 }
 
 // ---- SPARC row weights ---------------------------------------------------------------------
@@ -214,22 +304,35 @@ hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s) {
     return hipGetLastError();
 }
 
+int pacl_pool_splits(int R, int P) {
+    // >= 4096 workgroups (16 per CU) where the rows allow, >= 16 patches per workgroup
+    int S = (4096 + R - 1) / R;
+    const int smax = P / 16 > 1 ? P / 16 : 1;
+    return S < 1 ? 1 : S > smax ? smax : S;
+}
+
+size_t pacl_pool_part_bytes(int R, int P, int D) { return (size_t)R * pacl_pool_splits(R, P) * D * 4; }
+
 hipError_t launch_pacl_pool(const void* vp, bool vp_bf16, int Bi, int P, const float* tp, int Bt, int D,
                             int weight_mode, const float* rope_cos, const float* rope_sin, float* out_img,
-                            float* out_txt, hipStream_t s) {
-    if (D % 128 != 0 || D > 1024) return hipErrorInvalidValue;
+                            float* out_txt, float* part, hipStream_t s) {
+    if (D % 128 != 0 || D > 1024 || !part) return hipErrorInvalidValue;
     const int R = Bi > Bt ? Bi : Bt;
+    const int S = pacl_pool_splits(R, P);
     const bool rope = rope_cos != nullptr;
-    const dim3 grid(R), block(256);
+    const dim3 grid((unsigned)(R * S)), block(256);
+    bool launched = false;
 #define CE_PP(BF, MO, RO) \
-    if (vp_bf16 == BF && weight_mode == MO && rope == RO) { \
-        hipLaunchKernelGGL((pacl_pool_k<BF, MO, RO>), grid, block, 0, s, vp, Bi, P, tp, Bt, D, rope_cos, \
-                           rope_sin, out_img, out_txt); \
-        return hipGetLastError(); }
+    if (!launched && vp_bf16 == BF && weight_mode == MO && rope == RO) { \
+        hipLaunchKernelGGL((pacl_pool_part_k<BF, MO, RO>), grid, block, 0, s, vp, Bi, P, tp, Bt, D, rope_cos, \
+                           rope_sin, S, part); \
+        launched = true; }
     CE_PP(true, 0, false) CE_PP(true, 1, false) CE_PP(true, 1, true)
     CE_PP(false, 0, false) CE_PP(false, 1, false) CE_PP(false, 1, true)
 #undef CE_PP
-    return hipErrorInvalidValue;
+    if (!launched) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pacl_pool_finish_k, dim3((unsigned)R), block, 0, s, part, S, D, tp, Bt, out_img, out_txt);
+    return hipGetLastError();
 }
 
 hipError_t launch_sparc_weights(float* sim, long rows, int P, float sigma, hipStream_t s) {

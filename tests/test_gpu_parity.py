@@ -276,6 +276,36 @@ def test_pacl_pool_exact_vs_oracle(pacl_models):
     mod.weight_mode, mod.rope = open_clip_pacl_sigmoid.weight_mode, open_clip_pacl_sigmoid.rope
 
 
+@pytest.mark.parametrize("B,P,D,bf16", [(64, 576, 768, True), (5, 40, 1024, False), (2, 17, 128, True),
+                                         (512, 576, 768, True)])
+def test_pacl_pool_splits_vs_oracle(pacl_models, B, P, D, bf16):
+    """The two-pass pooling (pacl.py:120-145) at shapes that exercise its patch splits: many
+    splits per row (B = 64: 36 splits of 16 patches), ragged splits (P = 40, 17), D = 1024 and
+    D = 128 (partial 16-B chunk rounds), f32 and bf16 inputs, the C3 batch (B = 512, 8 splits),
+    and the Q6 broadcasts; vs the oracle on the same (bf16-rounded) values."""
+    mod = pacl_models["pacl_sigmoid"]
+    rng = np.random.default_rng(B + P + D)
+    vp = torch.from_numpy(rng.standard_normal((B, P, D)).astype(np.float32))
+    if bf16:
+        vp = vp.to(torch.bfloat16)
+    vpf = vp.float().numpy()
+    tp = rng.standard_normal((B, D)).astype(np.float32)
+    modes = [("ones", open_clip_pacl), ("sigmoid", open_clip_pacl_sigmoid)]
+    if P == 576 and D == 768:
+        modes.append(("sigmoid_rope", open_clip_pacl_rope_after))
+    try:
+        for bi, bt in ((B, B), (1, B), (B, 1)) if B <= 64 else ((B, B),):
+            for weights, cls in modes:
+                mod.weight_mode, mod.rope = cls.weight_mode, cls.rope
+                a, b = mod.pool(vp[:bi].cuda(), torch.from_numpy(tp[:bt]).cuda())
+                ra, rb = O.pacl_pool(vpf[:bi], tp[:bt], weights="ones" if weights == "ones" else "sigmoid",
+                                     rope_after=weights == "sigmoid_rope")
+                np.testing.assert_allclose(a.cpu().numpy(), ra, atol=2e-5, err_msg=f"{weights} {bi}x{bt}")
+                np.testing.assert_allclose(b.cpu().numpy(), rb, atol=2e-6)
+    finally:
+        mod.weight_mode, mod.rope = open_clip_pacl_sigmoid.weight_mode, open_clip_pacl_sigmoid.rope
+
+
 def test_apply_rope_vs_golden(pacl_models, golden):
     eng = pacl_models["pacl"].engine
     x = W.uniform("rope-input", 2 * 576 * 128).reshape(2, 576, 128)
