@@ -99,7 +99,7 @@ class Engine:
         return n.value, (first.value or b"").decode()
 
     def set_ln_fold(self, on: bool) -> bool:
-        """Fold the image tower's block LayerNorms into their GEMMs (default on); returns the previous
+        """Fold both towers' block LayerNorms into their GEMMs (default on); returns the previous
         setting.  Takes effect for weights already loaded in whole-block calls (ce_set_ln_fold)."""
         prev = ctypes.c_int()
         _lib.call("ce_set_ln_fold", self.h, 1 if on else 0, ctypes.byref(prev))

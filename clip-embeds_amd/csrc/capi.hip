@@ -526,11 +526,12 @@ bool fold_block(const ce_handle* h, const std::string& p, FoldBlk& f) {
     return f.wqkv && f.cqkv && f.dqkv && f.wfc && f.cfc && f.dfc;
 }
 
-// run_block with both pre-LNs folded into their GEMMs.  On entry w.xn = bf16(w.x) and w.stats =
-// (mu, rstd) of every row of w.x; the residual GEMMs re-establish both for the next block (the
-// last block of the tower skips that).
+// run_block with both pre-LNs folded into their GEMMs (either tower; the text tower's attention is
+// causal).  On entry w.xn = bf16(w.x) (with the hi/lo stream: the hi plane, w.xlo the lo plane) and
+// w.stats = (mu, rstd) of every row of w.x; the residual GEMMs re-establish both for the next block
+// (the last block of the tower writes f32 w.x instead).
 int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, const FoldBlk& f, int B, int L,
-                     int D, int H, int F, bool last) {
+                     int D, int H, int F, bool last, bool vis = true) {
     const int M = B * L;
     struct PartScope {
         ce_handle* h;
@@ -561,29 +562,30 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         last_ea.hl_plane = (long)M * D;
     }
     auto finalize = [&] {
-        return timed(h, s, "ln_stats_v", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
+        return timed(h, s, vis ? "ln_stats_v" : "ln_stats_t", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
                      [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s); });
     };
     fold.fold_c = f.cqkv;
-    CE_TRY(gemm(h, s, "gemm_qkv_v", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_, nullptr, w.qkv, true,
-                0, 0, 0, 0, 0, fold));
+    CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
+                nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
     {
         const double flops = 4.0 * B * H * (double)L * L * 64;
         const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
-        CE_TRY(timed(h, s, "attn_v", flops, bytes,
-                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, false, true, s); }));
+        CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
+                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, !vis, true, s); }));
     }
-    CE_TRY(gemm(h, s, "gemm_out_v", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, resid, w.x, false,
-                0, 0, 0, 0, 0, st));
+    CE_TRY(gemm(h, s, vis ? "gemm_out_v" : "gemm_out_t", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, resid,
+                w.x, false, 0, 0, 0, 0, 0, st));
     CE_TRY(finalize());
     fold.fold_c = f.cfc;
-    CE_TRY(gemm(h, s, "gemm_fc_v", w.xn, D, f.wfc, M, F, D, f.dfc, act_code(h), nullptr, w.hid, true,
-                0, 0, 0, 0, 0, fold));
+    CE_TRY(gemm(h, s, vis ? "gemm_fc_v" : "gemm_fc_t", w.xn, D, f.wfc, M, F, D, f.dfc, act_code(h), nullptr, w.hid,
+                true, 0, 0, 0, 0, 0, fold));
+    const char* tproj = vis ? "gemm_proj_v" : "gemm_proj_t";
     if (last) {
-        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
+        CE_TRY(gemm(h, s, tproj, w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
                     0, 0, 0, 0, 0, last_ea));
     } else {
-        CE_TRY(gemm(h, s, "gemm_proj_v", w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
+        CE_TRY(gemm(h, s, tproj, w.hid, F, k.wproj, M, D, F, k.bproj, ce::ACT_NONE_, resid, w.x, false,
                     0, 0, 0, 0, 0, st));
         CE_TRY(finalize());
     }
@@ -647,11 +649,29 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
              bool normalize) {
     const ce_config& c = h->cfg;
     const int D = c.text.width, L = c.context_length;
-    CE_TRY(check_launch(ce::launch_text_embed(w.x, ids, W(h, "token_embedding.weight"), W(h, "positional_embedding"),
-                                              B, L, D, c.vocab_size, s), "token_embedding"));
+    // LN folding as in the image tower: every block's fold current, D a multiple of 64
+    std::vector<FoldBlk> folds(c.text.layers);
+    bool use_fold = h->ln_fold && D % 64 == 0 && D / 64 <= 64 && c.text.layers > 0;
+    for (int i = 0; use_fold && i < c.text.layers; ++i)
+        use_fold = fold_block(h, "transformer.resblocks." + std::to_string(i) + ".", folds[i]);
+    if (use_fold) {
+        CE_TRY(timed(h, s, "t_embed", 0.0, (double)B * L * D * (h->resid_hl ? 12.0 : 10.0), [&] {
+            return ce::launch_text_embed_stats(w.x, w.xn, h->resid_hl ? w.xlo : nullptr, w.stats, ids,
+                                               W(h, "token_embedding.weight"), W(h, "positional_embedding"), B, L, D,
+                                               c.vocab_size, s);
+        }));
+    } else {
+        CE_TRY(check_launch(ce::launch_text_embed(w.x, ids, W(h, "token_embedding.weight"),
+                                                  W(h, "positional_embedding"), B, L, D, c.vocab_size, s),
+                            "token_embedding"));
+    }
     for (int i = 0; i < c.text.layers; ++i) {
         const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(i) + ".");
-        CE_TRY(run_block(h, s, w, k, B, L, D, c.text.heads, c.text.mlp_width, true, false));
+        if (use_fold)
+            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width,
+                                    i + 1 == c.text.layers, false));
+        else
+            CE_TRY(run_block(h, s, w, k, B, L, D, c.text.heads, c.text.mlp_width, true, false));
     }
     if (out_pooled) {
         CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
@@ -1160,8 +1180,11 @@ int ce_load_weights(ce_handle* h, const ce_tensor* t, int n, int allow_unknown) 
         CE_TRY(upload_named(h, name, bytes.data(), bytes.size()));
         h->loaded[name] = true;
     }
-    for (int l = 0; l < h->cfg.vision.layers; ++l) {
-        const std::string P = "visual.transformer.resblocks." + std::to_string(l) + ".";
+    // LN folds of both towers' blocks
+    std::vector<std::string> blocks;
+    for (int l = 0; l < h->cfg.vision.layers; ++l) blocks.push_back("visual.transformer.resblocks." + std::to_string(l) + ".");
+    for (int l = 0; l < h->cfg.text.layers; ++l) blocks.push_back("transformer.resblocks." + std::to_string(l) + ".");
+    for (const std::string& P : blocks) {
         CE_TRY(fold_linear(h, t, idx, P + "attn.in_proj_weight", P + "attn.in_proj_bias", P + "ln_1.weight",
                            P + "ln_1.bias", true));
         CE_TRY(fold_linear(h, t, idx, P + "mlp.c_fc.weight", P + "mlp.c_fc.bias", P + "ln_2.weight",
@@ -1942,6 +1965,10 @@ int ce_train_sync_weights(ce_handle* h, void* stream) {
                                                           ce::kAttnQScale, s), "weight_from_master"));
         h->loaded[kv.first] = true;
     }
+    // the trained tensors' LN folds (host-computed at ce_load_weights) are stale now: encode_text
+    // runs the unfolded text blocks until the tower is loaded again
+    for (auto& kv : h->folded)
+        if (kv.first.rfind("transformer.resblocks.", 0) == 0) kv.second = false;
     return CE_OK;
 }
 

@@ -110,6 +110,11 @@ hipError_t launch_cls_rows(float* x, const float* cls, const float* pos, int B, 
 // x[b*ctx+t][:] = tok[ids[b,t]] + pos[t]
 hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, const float* pos,
                              int B, int ctx, int D, int vocab, hipStream_t s);
+// the LN-folded text tower's entry state: x = tok[ids] + pos (f32), hi/lo bf16 planes (xlo may be
+// null: xb = bf16(x)), row (mu, rstd).  D in {256, 512, 768, 1024, 1280}.
+hipError_t launch_text_embed_stats(float* x, bf16_t* xb, bf16_t* xlo, float2* stats, const int64_t* ids,
+                                   const float* tok, const float* pos, int B, int ctx, int D, int vocab,
+                                   hipStream_t s);
 // rows[b] = b*ctx + argmax_t ids[b,t]  (first maximal id; EOT is the largest id)
 hipError_t launch_argmax_rows(int* rows, const int64_t* ids, int B, int ctx, hipStream_t s);
 // LayerNorm of gathered rows: out[i] = LN(x + rows[i]*row_stride) (f32); rows == nullptr -> rows[i] = i

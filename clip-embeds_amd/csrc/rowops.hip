@@ -194,6 +194,54 @@ __global__ __launch_bounds__(256) void text_embed_k(float* x, const int64_t* ids
     }
 }
 
+// Text embedding as the LN-folded text tower's entry state (the tower has no ln_pre): x = tok[id] +
+// pos (f32), its hi/lo bf16 planes (xb = hi, xlo = lo, optional) and the row (mu, rstd) that block
+// 0's folded QKV GEMM needs in place of ln_1.  One wave per row, D = NC * 256.
+template <int NC>
+__global__ __launch_bounds__(256) void text_embed_stats_k(float* __restrict__ x, bf16_t* __restrict__ xb,
+                                                          bf16_t* __restrict__ xlo, float2* __restrict__ stats,
+                                                          const int64_t* __restrict__ ids,
+                                                          const float* __restrict__ tok,
+                                                          const float* __restrict__ pos, int rows, int ctx,
+                                                          int vocab) {
+    constexpr int D = NC * 256;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    int64_t id = ids[row];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+    const float* tr = tok + (size_t)id * D;
+    const float* pr = pos + (size_t)(row % ctx) * D;
+    float4 v[NC];
+    float sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int e = c * 256 + lane * 4;
+        const float4 a = *reinterpret_cast<const float4*>(tr + e);
+        const float4 b = *reinterpret_cast<const float4*>(pr + e);
+        v[c] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+        sm += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+    }
+    const float mean = wave_sum(sm) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        q += ((v[c].x - mean) * (v[c].x - mean) + (v[c].y - mean) * (v[c].y - mean)) +
+             ((v[c].z - mean) * (v[c].z - mean) + (v[c].w - mean) * (v[c].w - mean));
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + 1e-5f);
+    if (lane == 0) stats[row] = make_float2(mean, rstd);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const size_t o = (size_t)row * D + c * 256 + lane * 4;
+        *reinterpret_cast<float4*>(x + o) = v[c];
+        uint2 hi, lo;
+        split_hl(v[c].x, v[c].y, hi.x, lo.x);
+        split_hl(v[c].z, v[c].w, hi.y, lo.y);
+        *reinterpret_cast<uint2*>(xb + o) = hi;
+        if (xlo) *reinterpret_cast<uint2*>(xlo + o) = lo;
+    }
+}
+
 __global__ __launch_bounds__(64) void argmax_rows_k(int* rows, const int64_t* ids, int B, int ctx) {
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
@@ -382,6 +430,21 @@ hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, con
                              int ctx, int D, int vocab, hipStream_t s) {
     if (D % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(text_embed_k, dim3(B * ctx), dim3(256), 0, s, x, ids, tok, pos, B, ctx, D, vocab);
+    return hipGetLastError();
+}
+
+hipError_t launch_text_embed_stats(float* x, bf16_t* xb, bf16_t* xlo, float2* stats, const int64_t* ids,
+                                   const float* tok, const float* pos, int B, int ctx, int D, int vocab,
+                                   hipStream_t s) {
+    const int rows = B * ctx;
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    if (!x || !xb || !stats) return hipErrorInvalidValue;
+    if (D == 768) hipLaunchKernelGGL(text_embed_stats_k<3>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    else if (D == 512) hipLaunchKernelGGL(text_embed_stats_k<2>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    else if (D == 1024) hipLaunchKernelGGL(text_embed_stats_k<4>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    else if (D == 1280) hipLaunchKernelGGL(text_embed_stats_k<5>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    else if (D == 256) hipLaunchKernelGGL(text_embed_stats_k<1>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -311,14 +311,15 @@ int ce_set_gemm_trace(void* buf, int64_t n_blocks);
 /* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
  * stats [rows] float2, part [rows][nslab] float2. */
 int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab);
-/* LayerNorm folding of the image tower (default on; env CE_LN_FOLD=0 turns it off at ce_create):
- * ln_1/ln_2 of every visual block are folded into the in_proj/c_fc weights at ce_load_weights,
- * and the residual GEMMs emit the row statistics, so no LayerNorm launch remains inside the
- * blocks.  Needs each block's in_proj/c_fc weight+bias and ln_1/ln_2 loaded in
- * one ce_load_weights call; otherwise the unfolded path runs.  *previous (may be null) gets the
- * previous setting. */
+/* LayerNorm folding of both towers (default on; env CE_LN_FOLD=0 turns it off at ce_create):
+ * ln_1/ln_2 of every block are folded into the in_proj/c_fc weights at ce_load_weights, and the
+ * residual GEMMs emit the row statistics, so no LayerNorm launch remains inside the blocks
+ * (the text tower's entry state comes from the token-embedding kernel).  Needs each
+ * block's in_proj/c_fc weight+bias and ln_1/ln_2 loaded in one ce_load_weights call; otherwise
+ * that tower runs unfolded (also the text tower after ce_train_sync_weights, until it is loaded
+ * again).  *previous (may be null) gets the previous setting. */
 int ce_set_ln_fold(ce_handle* h, int enable, int* previous);
-/* Residual stream of the LN-folded image tower as two bf16 planes (default on; env CE_RESID_HL=0 at
+/* Residual stream of the LN-folded towers as two bf16 planes (default on; env CE_RESID_HL=0 at
  * ce_create): inside the blocks the out-proj / c_proj GEMMs read x = hi + lo and write hi = bf16(x),
  * lo = bf16(x - hi) (hi doubles as the folded GEMMs' bf16 operand) instead of f32 x plus its bf16
  * copy: 4 B per element written instead of 6; |x - (hi + lo)| <= 2^-17 |x|.  The tower's last

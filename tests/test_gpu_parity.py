@@ -213,6 +213,62 @@ def test_ln_fold_matches_unfolded():
         m.visual.output_tokens = False
 
 
+def _ran_text_folded(m, fn):
+    e = m._engine
+    e.set_timing(True)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        names = {k["name"] for k in e.kernel_stats()}
+    finally:
+        e.set_timing(False)
+    return out, "ln_stats_t" in names and "ln_t" not in names
+
+
+def test_text_ln_fold_matches_unfolded():
+    """Text tower with ln_1/ln_2 folded into in_proj/c_fc and its residual stream as hi/lo planes
+    (default, as the image tower) vs the LayerNorm path, full depth, causal blocks: pooled and
+    token outputs within 2e-4 cosine of each other and within 1e-3 of the golden reference; the
+    f32-stream fold agrees to 1e-5; a partial reload of one LN weight runs the unfolded text blocks
+    with the new weight."""
+    cfg = get_model_config("ViT-L-14-336")
+    m = make_model(cfg)
+    caps = torch.from_numpy(W.synthetic_captions(5, seed=77))
+    m.output_text_tokens = True
+    try:
+        (pf, tf), folded = _ran_text_folded(m, lambda: m.encode_text(caps))
+        assert folded
+        prev = m._engine.set_resid_hl(False)
+        try:
+            (ph, th), folded = _ran_text_folded(m, lambda: m.encode_text(caps))
+            assert folded
+        finally:
+            m._engine.set_resid_hl(prev)
+        assert cos_dist(pf.cpu().numpy(), ph.cpu().numpy()) < 1e-5
+        m._engine.set_ln_fold(False)
+        try:
+            (pu, tu), folded = _ran_text_folded(m, lambda: m.encode_text(caps))
+            assert not folded
+        finally:
+            m._engine.set_ln_fold(True)
+        assert cos_dist(pf.cpu().numpy(), pu.cpu().numpy()) < 2e-4
+        assert cos_dist(tf.cpu().numpy().reshape(-1, 768), tu.cpu().numpy().reshape(-1, 768)) < 2e-4
+        sd = W.synthetic_state_dict(cfg)
+        o = O.encode_text(sd, caps.numpy(), cfg)
+        assert cos_dist(pf.cpu().numpy(), o) < COS_TOL
+        k = "transformer.resblocks.5.ln_1.bias"
+        b2 = torch.from_numpy(sd[k] + 0.5)
+        m.load_state_dict({k: b2})
+        (p2, _), folded = _ran_text_folded(m, lambda: m.encode_text(caps))
+        assert not folded
+        sd2 = dict(sd)
+        sd2[k] = b2.numpy()
+        assert cos_dist(p2.cpu().numpy(), O.encode_text(sd2, caps.numpy(), cfg)) < COS_TOL
+        m.load_state_dict({k: torch.from_numpy(sd[k])})
+    finally:
+        m.output_text_tokens = False
+
+
 @pytest.fixture(scope="module")
 def pacl_models():
     cfg = get_model_config("ViT-L-14-336").with_depth(2, 2)

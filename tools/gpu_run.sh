@@ -5,6 +5,8 @@
 #   smoke                                  __graft_entry__.smoke()
 #   bench:<bench.py args, comma-separated> one bench.py run (JSON line -> gpurun_out/TAG_benchN.log)
 #   rocprof:<bench.py args>                rocprofv3 --kernel-trace --stats of one bench.py run
+#   clock:<bench.py args>                  GRBM_GUI_ACTIVE pass (effective clock per kernel)
+#   pmc:<counter>,<bench.py args>          one --pmc pass with one counter over a short bench run
 # Every step has its own time limit; the chain stops at the first failure.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -23,6 +25,13 @@ for step in "$@"; do
     bench)   timeout -k 10 400 python -u bench.py $args > gpurun_out/${TAG}_bench$n.log 2>&1 ;;
     rocprof) timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$n -o run -- \
                python3 -u bench.py --no-cpu-baseline $args > gpurun_out/${TAG}_prof$n.log 2>&1 ;;
+    clock)   timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/${TAG}_clk$n \
+               -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-timing $args \
+               > gpurun_out/${TAG}_clk$n.log 2>&1 ;;
+    pmc)     cnt=${args%% *}; rest=${args#* }; [ "$rest" = "$args" ] && rest=""
+             timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $cnt -d gpurun_out/${TAG}_pmc${n}_$cnt \
+               -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-timing $rest \
+               > gpurun_out/${TAG}_pmc${n}.log 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
