@@ -76,6 +76,7 @@ constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a 
 // kernel scales its Q fragments.
 constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(64)
 int set_attn_variant(int var);  // attention forward variant (0-2) for A/B; returns previous
+int set_fgemm_variant(int v);   // 1 = register-blocked f32 GEMM (default), 0 = the 64 x 64 kernel
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse = nullptr);   // lse: [B][H][L] log2 log-sum-exp (training)
 

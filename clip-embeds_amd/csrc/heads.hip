@@ -78,6 +78,117 @@ __global__ __launch_bounds__(256) void fgemm_k(FGemmParams p) {
     }
 }
 
+// ---- register-blocked f32 GEMM (the SPARC einsums, projections, logits) ----------------------
+// 96 x 128 output tile per 256-thread block: wave w owns columns 32w .. 32w+31 and all 96 rows as
+// three 32 x 32 accumulators, so one B fragment feeds three v_mfma_f32_32x32x2_f32.  K chunks of 32
+// are staged global -> registers (float4) -> LDS, the next chunk's loads in flight under the current
+// chunk's MFMAs.  LDS image: [k parity][row][k / 2] with rows padded to 20 floats, so a lane's 4
+// consecutive k-pairs come in one ds_read_b128 (lane l: row l & 31, parity l >> 5) and the 16 lanes
+// of a read group hit distinct banks.  96 rows: M = 77 (SPARC's T) fills 80 % of the MFMA rows.
+constexpr int G2_BM = 96, G2_BN = 128, G2_BK = 32, G2_LD = G2_BK / 2 + 4;
+
+template <bool B_NK>
+__global__ __launch_bounds__(256) void fgemm2_k(FGemmParams p) {
+    __shared__ __attribute__((aligned(16))) float As[2][G2_BM][G2_LD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][G2_BN][G2_LD];
+    const int z = blockIdx.z;
+    const float* A = p.A + (size_t)z * p.sA;
+    const float* Bm = p.B + (size_t)z * p.sB;
+    float* C = p.C + (size_t)z * p.sC;
+    const int i0 = blockIdx.y * G2_BM, j0 = blockIdx.x * G2_BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    f32x16 acc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+    // staging: A chunk = 96 rows x 32 k = 768 float4 (3 per thread); B chunk = 128 x 32 = 1024
+    // float4 (4 per thread), [n][k] rows when B_NK, else [k][n] rows
+    float4 ra[3], rb[4];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, kq = (e & 7) * 4;
+            const int gi = i0 + row, gk = k0 + kq;
+            ra[u] = (gi < p.M && gk < p.K) ? *reinterpret_cast<const float4*>(A + (size_t)gi * p.lda + gk)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + 256 * u;
+            if constexpr (B_NK) {
+                const int row = e >> 3, kq = (e & 7) * 4;
+                const int gj = j0 + row, gk = k0 + kq;
+                rb[u] = (gj < p.N && gk < p.K) ? *reinterpret_cast<const float4*>(Bm + (size_t)gj * p.ldb + gk)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                const int kk = e >> 5, nq = (e & 31) * 4;
+                const int gj = j0 + nq, gk = k0 + kk;
+                rb[u] = (gj < p.N && gk < p.K) ? *reinterpret_cast<const float4*>(Bm + (size_t)gk * p.ldb + gj)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto store = [&] {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, kp = (e & 7) * 2;
+            *reinterpret_cast<float2*>(&As[0][row][kp]) = make_float2(ra[u].x, ra[u].z);
+            *reinterpret_cast<float2*>(&As[1][row][kp]) = make_float2(ra[u].y, ra[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + 256 * u;
+            if constexpr (B_NK) {
+                const int row = e >> 3, kp = (e & 7) * 2;
+                *reinterpret_cast<float2*>(&Bs[0][row][kp]) = make_float2(rb[u].x, rb[u].z);
+                *reinterpret_cast<float2*>(&Bs[1][row][kp]) = make_float2(rb[u].y, rb[u].w);
+            } else {
+                const int kk = e >> 5, nq = (e & 31) * 4;
+                float* d = &Bs[kk & 1][nq][kk >> 1];
+                d[0] = rb[u].x; d[G2_LD] = rb[u].y; d[2 * G2_LD] = rb[u].z; d[3 * G2_LD] = rb[u].w;
+            }
+        }
+    };
+    const int h = lane >> 5, m = lane & 31;
+    load(0);
+    for (int k0 = 0; k0 < p.K; k0 += G2_BK) {
+        store();
+        __syncthreads();
+        if (k0 + G2_BK < p.K) load(k0 + G2_BK);
+#pragma unroll
+        for (int q = 0; q < G2_BK / 8; ++q) {      // 4 k-pairs per ds_read_b128
+            const float4 b4 = *reinterpret_cast<const float4*>(&Bs[h][wave * 32 + m][4 * q]);
+            float4 a4[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) a4[r] = *reinterpret_cast<const float4*>(&As[h][r * 32 + m][4 * q]);
+            const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const float aq[4] = {a4[r].x, a4[r].y, a4[r].z, a4[r].w};
+                    acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[kk], bq[kk], acc[r], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int gj = j0 + wave * 32 + m;
+    if (gj >= p.N) return;
+    const float bj = p.bias ? p.bias[gj] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int gi = i0 + r * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (gi >= p.M) continue;
+            const float v = acc[r][e] * p.alpha + bj;
+            C[(size_t)gi * p.ldc + gj] = v;
+            if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
+        }
+}
+
 // ---- fused PACL pooling -----------------------------------------------------------------
 // Two passes.  Pass 1 (pacl_pool_part_k): grid = R output rows x S patch splits; each 256-thread
 // workgroup streams its P/S patches of one image, one patch row per wave at a time, every lane
@@ -294,10 +405,29 @@ __global__ __launch_bounds__(256) void sparc_weights_k(float* sim, long rows, in
     for (int p = lane; p < P; p += 64) r[p] = r[p] / s;
 }
 
+int g_fgemm2 = 1;     // register-blocked f32 GEMM (0: the 64 x 64 scalar-staged kernel, for A/B)
+
 }  // namespace
+
+int set_fgemm_variant(int v) {
+    const int prev = g_fgemm2;
+    g_fgemm2 = v != 0;
+    return prev;
+}
 
 hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s) {
     if (p.M <= 0 || p.N <= 0 || p.batch <= 0) return hipSuccess;
+    // float4 staging needs 16-B aligned rows and K chunks: every operand base, stride and K a
+    // multiple of 4 floats; anything else takes the scalar-staged 64 x 64 kernel
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    const bool vec = p.K % 4 == 0 && p.lda % 4 == 0 && p.ldb % 4 == 0 && p.sA % 4 == 0 && p.sB % 4 == 0 &&
+                     al(p.A) && al(p.B) && (b_nk || p.N % 4 == 0);
+    if (vec && g_fgemm2) {
+        const dim3 grid((p.N + G2_BN - 1) / G2_BN, (p.M + G2_BM - 1) / G2_BM, p.batch);
+        if (b_nk) hipLaunchKernelGGL(fgemm2_k<true>, grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(fgemm2_k<false>, grid, dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     const dim3 grid((p.N + FT - 1) / FT, (p.M + FT - 1) / FT, p.batch);
     if (b_nk) hipLaunchKernelGGL(fgemm_k<true>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(fgemm_k<false>, grid, dim3(256), 0, s, p);

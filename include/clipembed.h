@@ -286,6 +286,10 @@ int ce_set_gemm_variant(int bits);
  * (default); anything else restores the default.  Causal launches (text tower) use mode 0 with bit 8
  * when set.  Returns the previous variant. */
 int ce_set_attn_variant(int var);
+/* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
+ * register-blocked 96 x 128 kernel (default, for 16-B aligned operands with K % 4 == 0), 0 = the
+ * 64 x 64 scalar-staged kernel.  Returns the previous setting.  For A/B and parity tests. */
+int ce_set_fgemm_variant(int v);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
  * schedules, 10 = two-workgroup 256 x 128 (SCHED 12), and epi 0 = plain, 1 = LN statistics, 2 = LN
