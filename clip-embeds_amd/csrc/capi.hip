@@ -1254,7 +1254,7 @@ int ce_encode_text(ce_handle* h, void* stream, const int64_t* ids, int B, int ct
     TowerWs w = carve(h->ws_t, (long)B * ctx, D, h->cfg.text.mlp_width, 0, B);
     CE_TRY(run_text(h, s, w, ids, B, out_pooled, normalize != 0));
     if (out_tokens)
-        CE_TRY(layernorm(h, s, "ln_t", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "ln_final.weight"),
+        CE_TRY(layernorm(h, s, "ln_final_t", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "ln_final.weight"),
                          W(h, "ln_final.bias"), B * ctx, D));
     return CE_OK;
 }
