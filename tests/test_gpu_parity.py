@@ -244,7 +244,10 @@ def test_text_ln_fold_matches_unfolded():
             assert folded
         finally:
             m._engine.set_resid_hl(prev)
-        assert cos_dist(pf.cpu().numpy(), ph.cpu().numpy()) < 1e-5
+        # 12 random-init causal blocks amplify the rare 1-ulp bf16 flips of the GEMM operand that the
+        # two streams' residuals (f32 vs hi + lo, |x - (hi + lo)| <= 2^-16 |x|) cause; one block shows
+        # the per-block agreement (test_text_resid_hl_one_block)
+        assert cos_dist(pf.cpu().numpy(), ph.cpu().numpy()) < 3e-5
         m._engine.set_ln_fold(False)
         try:
             (pu, tu), folded = _ran_text_folded(m, lambda: m.encode_text(caps))
@@ -265,6 +268,29 @@ def test_text_ln_fold_matches_unfolded():
         sd2[k] = b2.numpy()
         assert cos_dist(p2.cpu().numpy(), O.encode_text(sd2, caps.numpy(), cfg)) < COS_TOL
         m.load_state_dict({k: torch.from_numpy(sd[k])})
+    finally:
+        m.output_text_tokens = False
+
+
+def test_text_resid_hl_one_block():
+    """One folded text block: the hi/lo residual planes (written by the embedding kernel, updated
+    by the out-proj GEMM) vs the f32 stream agree to the planes' 2^-16 representation error, far
+    below what a missing lo plane (2^-9) would show."""
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    m = make_model(cfg)
+    caps = torch.from_numpy(W.synthetic_captions(8, seed=78))
+    m.output_text_tokens = True
+    try:
+        ph, th = m.encode_text(caps)
+        prev = m._engine.set_resid_hl(False)
+        try:
+            pf, tf = m.encode_text(caps)
+        finally:
+            m._engine.set_resid_hl(prev)
+        assert cos_dist(th.cpu().numpy().reshape(-1, 768), tf.cpu().numpy().reshape(-1, 768)) < 1e-8
+        assert cos_dist(ph.cpu().numpy(), pf.cpu().numpy()) < 1e-8
+        o = O.encode_text(W.synthetic_state_dict(cfg), caps.numpy(), cfg)
+        assert cos_dist(ph.cpu().numpy(), o) < COS_TOL
     finally:
         m.output_text_tokens = False
 
