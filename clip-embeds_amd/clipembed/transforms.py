@@ -150,14 +150,20 @@ def image_transform(image_size=336, is_train: bool = False, mean: Optional[Seque
     if is_train:
         # open_clip's default AugmentationCfg (transform.py:62-72,334-355); jitter / grayscale / timm
         # augmentations are not on the device path
+        # RandomResizedCrop gets `scale` only (transform.py:334-340): a `ratio` in aug_cfg is one of
+        # the "Unused augmentation cfg items" the reference warns about (:356-357), so the default
+        # (3/4, 4/3) stays and the seeded boxes match the reference's
         scale, ratio = (0.9, 1.0), (3.0 / 4.0, 4.0 / 3.0)
         if aug_cfg is not None:
             cfg = aug_cfg if isinstance(aug_cfg, dict) else vars(aug_cfg)
-            extra = {k for k, v in cfg.items() if v and k not in ("scale", "ratio")}
-            if extra:
-                raise NotImplementedError(f"training augmentations {sorted(extra)} are not on the device path")
+            extra = {k for k, v in cfg.items() if v and k not in ("scale", "ratio", "use_timm")}
+            if extra or cfg.get("use_timm"):
+                raise NotImplementedError(f"training augmentations {sorted(extra | ({'use_timm'} if cfg.get('use_timm') else set()))} "
+                                          "are not on the device path")
             scale = tuple(cfg.get("scale") or scale)
-            ratio = tuple(cfg.get("ratio") or ratio)
+            if cfg.get("ratio"):
+                import warnings
+                warnings.warn("Unused augmentation cfg items, specify `use_timm` to use (['ratio']).")
         if (mean is not None and tuple(mean) != tuple(OPENAI_MEAN)) or (std is not None and tuple(std) != tuple(OPENAI_STD)):
             raise NotImplementedError("the device path normalises with the OpenAI mean/std (constants.py:1-2)")
         return DeviceTrainProcessor(image_size, scale, ratio, device, engine=engine)

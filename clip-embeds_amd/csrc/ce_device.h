@@ -28,7 +28,7 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 }
 
 // Residual stream as two bf16 planes (EPI_LN_STATS_HL): hi = bf16(v), lo = bf16(v - hi); hi + lo
-// keeps ~16 significand bits (|v - (hi + lo)| <= 2^-17 |v|) in 4 bytes, and hi is exactly the bf16
+// keeps ~16 significand bits (|v - (hi + lo)| <= 2^-16 |v|: 2^-8 of v for hi, 2^-8 of that for lo) in 4 bytes, and hi is exactly the bf16
 // copy the LN-folded GEMMs read as their A operand.
 __device__ __forceinline__ void split_hl(float a, float b, uint32_t& hi, uint32_t& lo) {
     hi = pack_bf2(a, b);

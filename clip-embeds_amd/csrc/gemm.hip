@@ -118,7 +118,10 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        // the four-wave schedule with one tile per workgroup (grid = tiles): an exiting workgroup's
        // stores drain while the next one on the CU starts, instead of ahead of the next tile's DMAs
        GEMM_VAR_W4_ONETILE = 16,
-       // split-K tail on the four-wave persistent schedule (a last round of <= 1/8 of the grid)
+       // split-K tail on the four-wave persistent schedule (a last round of <= 1/8 of the grid).
+       // Off by default; with EPI2 on a GELU GEMM its tail tiles finish in gemm_splitk_fixup with the
+       // polynomial GELU (gelu_pair, <= 2.5e-6) while the main tiles use gelu_fast4 (<= 6.2e-5):
+       // both far inside the bf16 output rounding, but A/B timings of this bit mix two epilogues
        GEMM_VAR_W4_TAIL = 32,
        // timing ablation of the LN-statistics epilogues: no bf16 copy of the output (wrong xb)
        GEMM_VAR_ABL_NOXB = 64,

@@ -310,7 +310,9 @@ int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, i
                             void* stats_part, const void* fold_stats, const float* fold_c);
 /* Diagnostics: when buf (device, n_blocks x 4 uint64) is non-null, the SCHED 1 / SCHED 12 GEMM
  * kernels record per workgroup {s_memrealtime at start, after the K-loop, after wave 0's epilogue,
- * (XCC id << 32) | HW_ID} for blocks < n_blocks.  Null turns it off. */
+ * (XCC id << 32) | HW_ID} for blocks < n_blocks.  Null turns it off.  The pointer is process-wide
+ * and every later GEMM launch of every handle and stream writes through it: diagnostics only, one
+ * stream at a time, and call ce_set_gemm_trace(NULL, 0) (after a sync) before freeing buf. */
 int ce_set_gemm_trace(void* buf, int64_t n_blocks);
 /* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
  * stats [rows] float2, part [rows][nslab] float2. */
@@ -326,7 +328,7 @@ int ce_set_ln_fold(ce_handle* h, int enable, int* previous);
 /* Residual stream of the LN-folded towers as two bf16 planes (default on; env CE_RESID_HL=0 at
  * ce_create): inside the blocks the out-proj / c_proj GEMMs read x = hi + lo and write hi = bf16(x),
  * lo = bf16(x - hi) (hi doubles as the folded GEMMs' bf16 operand) instead of f32 x plus its bf16
- * copy: 4 B per element written instead of 6; |x - (hi + lo)| <= 2^-17 |x|.  The tower's last
+ * copy: 4 B per element written instead of 6; |x - (hi + lo)| <= 2^-16 |x|.  The tower's last
  * residual GEMM writes f32 x.  *previous (may be null) gets the previous setting. */
 int ce_set_resid_hl(ce_handle* h, int enable, int* previous);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */

@@ -151,7 +151,7 @@ def _ran_folded(m, fn):
 def test_resid_hl_matches_f32_stream():
     """The folded image tower with its residual stream as hi/lo bf16 planes (default) vs the f32
     stream + bf16 copy, full depth: pooled and token outputs within 1e-5 cosine of each other
-    (|x - (hi + lo)| <= 2^-17 |x| per residual GEMM) and within 1e-3 of the golden."""
+    (|x - (hi + lo)| <= 2^-16 |x| per residual GEMM) and within 1e-3 of the golden."""
     cfg = get_model_config("ViT-L-14-336")
     m = make_model(cfg)
     imgs = torch.from_numpy(W.synthetic_images(3, seed=98))

@@ -109,3 +109,17 @@ def test_gelu_sigmoid_error_bound():
     g = (x * r).astype(np.float32)
     ref = 0.5 * x.astype(np.float64) * (1 + erf(x.astype(np.float64) / np.sqrt(2)))
     assert (np.abs(g - ref) / np.maximum(1.0, np.abs(ref))).max() <= 6.5e-5
+
+
+def test_train_transform_ignores_ratio_like_reference():
+    """open_clip's non-timm train transform passes only `scale` to RandomResizedCrop and warns
+    about any other aug_cfg item (transform.py:334-357): a `ratio` leaves the default (3/4, 4/3)."""
+    from clipembed.transforms import DeviceTrainProcessor, image_transform
+    with pytest.warns(UserWarning, match="Unused augmentation cfg items"):
+        t = image_transform(336, is_train=True, aug_cfg={"scale": (0.5, 1.0), "ratio": (0.5, 2.0)})
+    assert isinstance(t, DeviceTrainProcessor)
+    assert t.scale == (0.5, 1.0) and t.ratio == (3.0 / 4.0, 4.0 / 3.0)
+    with pytest.raises(NotImplementedError):
+        image_transform(336, is_train=True, aug_cfg={"color_jitter_prob": 0.5})
+    with pytest.raises(NotImplementedError):
+        image_transform(336, is_train=True, aug_cfg={"use_timm": True})
