@@ -7,6 +7,8 @@
 #   rocprof:<bench.py args>                rocprofv3 --kernel-trace --stats of one bench.py run
 #   clock:<bench.py args>                  GRBM_GUI_ACTIVE pass (effective clock per kernel)
 #   pmc:<counter>,<bench.py args>          one --pmc pass with one counter over a short bench run
+#   py:<script>,<args>                     any python script (kernel A/B: tools/bench_gemm_epi.py,
+#                                          tools/bench_kernels.py; timelines: tools/gemm_trace.py)
 # Every step has its own time limit; the chain stops at the first failure.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -32,6 +34,7 @@ for step in "$@"; do
              timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $cnt -d gpurun_out/${TAG}_pmc${n}_$cnt \
                -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-timing $rest \
                > gpurun_out/${TAG}_pmc${n}.log 2>&1 ;;
+    py)      timeout -k 10 600 python -u $args > gpurun_out/${TAG}_py$n.log 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
