@@ -274,8 +274,11 @@ def test_text_ln_fold_matches_unfolded():
 
 def test_text_resid_hl_one_block():
     """One folded text block: the hi/lo residual planes (written by the embedding kernel, updated
-    by the out-proj GEMM) vs the f32 stream agree to the planes' 2^-16 representation error, far
-    below what a missing lo plane (2^-9) would show."""
+    by the out-proj GEMM) vs the f32 stream.  The text residual stream is small (token + positional
+    embeddings, std ~0.02), so the LN fold's rstd (~50) magnifies the rare 1-ulp flips of bf16(x)
+    that the two representations cause: measured 7.0e-7 token cosine distance between them vs
+    2.7e-5 for either against the f32 oracle (the unfolded LayerNorm path: 2.4e-5;
+    tools/diag_text_fold.py)."""
     cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
     m = make_model(cfg)
     caps = torch.from_numpy(W.synthetic_captions(8, seed=78))
@@ -287,10 +290,11 @@ def test_text_resid_hl_one_block():
             pf, tf = m.encode_text(caps)
         finally:
             m._engine.set_resid_hl(prev)
-        assert cos_dist(th.cpu().numpy().reshape(-1, 768), tf.cpu().numpy().reshape(-1, 768)) < 1e-8
-        assert cos_dist(ph.cpu().numpy(), pf.cpu().numpy()) < 1e-8
-        o = O.encode_text(W.synthetic_state_dict(cfg), caps.numpy(), cfg)
+        assert cos_dist(th.cpu().numpy().reshape(-1, 768), tf.cpu().numpy().reshape(-1, 768)) < 5e-6
+        assert cos_dist(ph.cpu().numpy(), pf.cpu().numpy()) < 5e-6
+        o, ot = O.encode_text(W.synthetic_state_dict(cfg), caps.numpy(), cfg, output_tokens=True)
         assert cos_dist(ph.cpu().numpy(), o) < COS_TOL
+        assert cos_dist(th.cpu().numpy(), ot) < 1e-4
     finally:
         m.output_text_tokens = False
 
