@@ -37,6 +37,14 @@ constexpr int STAGE_BYTES = 2 * TILE_KV_BYTES;      // K + V
 __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((CE_LDS s16x4*)(p));
 }
+// The same read as inline asm: with the builtin, hipcc waits vmcnt(0) before it (it cannot tell the
+// V tile being read from the next tile's LDS-DMA in flight), so every key tile waited for its
+// successor's K/V transfer in the middle of its P.V MFMAs.  The caller waits lgkmcnt itself.
+__device__ __forceinline__ s16x4 ds_read_tr16_asm(const char* p) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((unsigned)(uintptr_t)(CE_LDS void*)p));
+    return r;
+}
 
 __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
@@ -60,6 +68,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
     constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
+    constexpr bool ASMV = (VAR & 16) != 0;   // V^T reads by inline asm (no vmcnt(0) before P.V)
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -155,6 +164,49 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     float l_run = 0.f;   // partial (this half's keys)
     bool fast = false;   // wave-uniform: softmax offset fixed at 0 (MODE >= 1)
     const f32x16 zero16 = {};
+
+    // O^T += V^T P^T with the V^T fragments read by inline asm (no wait on the LDS-DMA in flight):
+    // the reads of 16-key group q + 1 are issued before the MFMAs of group q, counted lgkmcnt.
+    // Addresses: one lane base per dt (smem + voff[dt]) plus compile-time immediates (VB = the V
+    // tile of ring slot BUF), so the reads need no address VGPRs of their own.
+    unsigned vaddr[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) vaddr[dt] = (unsigned)(uintptr_t)(CE_LDS void*)(smem + voff[dt]);
+    auto pv_asm = [&](auto vbc, const bf16x8 (&pf)[2][2], bool with_half2) {
+        constexpr int VB = decltype(vbc)::value;
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x4 vr[2][2][2];        // [ring][dt][lo, hi]
+#define CE_TRV(R, DT, H, OFF) \
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[R][DT][H]) : "v"(vaddr[DT]), "n"(OFF))
+#define CE_ISSUE(Q) \
+    CE_TRV((Q) & 1, 0, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
+    CE_TRV((Q) & 1, 0, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024); \
+    CE_TRV((Q) & 1, 1, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
+    CE_TRV((Q) & 1, 1, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024)
+        auto mf = [&](int q) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[q >> 1][q & 1],
+                                                               o[dt], 0, 0, 0);
+            }
+        };
+        // one 16-key group at a time (issuing the next group ahead holds 16 more VGPRs: 156 > 128,
+        // three waves per SIMD instead of four); the other waves on the SIMD cover the LDS latency
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q >= 2 && !with_half2) break;
+            if (q == 0) { CE_ISSUE(0); }
+            else if (q == 1) { CE_ISSUE(1); }
+            else if (q == 2) { CE_ISSUE(2); }
+            else { CE_ISSUE(3); }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            mf(q);
+        }
+#undef CE_ISSUE
+#undef CE_TRV
+    };
 
     // O^T += V^T P^T for the tile's P fragments (pf[kt2][s2]: keys kt2*32 + 16*s2 .. +15)
     auto pv = [&](const char* vb, const bf16x8 (&pf)[2][2], bool with_half2, bool rowsum) {
@@ -274,7 +326,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                     l_run += psum;
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                pv(vb, pf, true, MODE == 2);
+                if constexpr (ASMV && MODE != 2)
+                    pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, true);
+                else
+                    pv(vb, pf, true, MODE == 2);
             } else {
                 // rare: the tile is redone on the general path below (exact row max, rescale),
                 // and the wave stays there
@@ -347,7 +402,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                         pf[kt2][s2][j] = (__bf16)pv_;
                     }
             l_run += psum;
-            pv(vb, pf, half2, false);
+            if constexpr (ASMV)
+                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, half2);
+            else
+                pv(vb, pf, half2, false);
         }
         if (!ONEBAR) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -410,9 +468,13 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var;
     if (causal) {
-        if (v & 8) CE_ATTN_LAUNCH(true, 8); else CE_ATTN_LAUNCH(true, 0);
+        if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
+        else if (v & 8) CE_ATTN_LAUNCH(true, 8);
+        else CE_ATTN_LAUNCH(true, 0);
     } else {
         switch (v) {
+            case 29: CE_ATTN_LAUNCH(false, 29); break;
+            case 16: CE_ATTN_LAUNCH(false, 16); break;
             case 0: CE_ATTN_LAUNCH(false, 0); break;
             case 2: CE_ATTN_LAUNCH(false, 2); break;
             case 5: CE_ATTN_LAUNCH(false, 5); break;
@@ -428,7 +490,8 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
-    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13) ? var : 13;
+    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29)
+                     ? var : 13;
     return prev;
 }
 

@@ -8,7 +8,9 @@ by tests/golden/make_golden_eval.py).
 Decision margins (logit units: 100 x cosine difference, or log-odds) are reported.  A decision
 must match the reference unless the reference margin is inside the numerical tie band TIE, and
 every margin must agree with the reference's within MARGIN_TOL (the bf16 engine vs the f32
-reference: features within 1e-3 cosine distance move a 100-scaled logit by well under this)."""
+reference: features within 1e-3 cosine distance move a 100-scaled logit by well under this).
+40 items (20 MMVP pairs = 40 MMVP decisions): at least MIN_ASSERTED decisions of every kind lie
+outside the tie band and are asserted identical."""
 import importlib.util
 import os
 
@@ -28,6 +30,7 @@ _spec2 = importlib.util.spec_from_file_location("mge", os.path.join(HERE, "golde
 
 MARGIN_TOL = 0.1
 TIE = 2 * MARGIN_TOL
+MIN_ASSERTED = 8
 
 
 def _items():
@@ -68,7 +71,10 @@ def _check(name, got_margin, ref_margin, got_dec, ref_dec):
           f"max |diff| {d.max():.4f}, ties {int(ties.sum())}")
     assert d.max() < MARGIN_TOL, f"{name}: margin differs by {d.max()}"
     got_dec, ref_dec = np.asarray(got_dec), np.asarray(ref_dec)
+    assert int((~ties).sum()) >= MIN_ASSERTED, f"{name}: only {int((~ties).sum())} decisions outside the tie band"
     assert np.array_equal(got_dec[~ties], ref_dec[~ties]), f"{name}: decisions {got_dec} vs {ref_dec}"
+    print(f"{name}: {int((~ties).sum())} decisions asserted identical, "
+          f"{int((got_dec == ref_dec).sum())}/{got_dec.size} identical overall")
     return int((got_dec == ref_dec).sum()), got_dec.size
 
 

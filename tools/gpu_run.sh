@@ -25,7 +25,7 @@ for step in "$@"; do
                > gpurun_out/${TAG}_gputests.log 2>&1 ;;
     smoke)   timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     bench)   timeout -k 10 400 python -u bench.py $args > gpurun_out/${TAG}_bench$n.log 2>&1 ;;
-    rocprof) timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$n -o run -- \
+    rocprof) timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$n -o run --output-format csv -- \
                python3 -u bench.py --no-cpu-baseline $args > gpurun_out/${TAG}_prof$n.log 2>&1 ;;
     clock)   timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/${TAG}_clk$n \
                -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-timing $args \
