@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
     constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
     constexpr bool ASMV = (VAR & 16) != 0;   // V^T reads by inline asm (no vmcnt(0) before P.V)
+    constexpr bool FAST0 = (VAR & 32) != 0;  // tile 0 on the fixed offset too (two-sided check)
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -162,7 +163,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
     float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
     float l_run = 0.f;   // partial (this half's keys)
-    bool fast = false;   // wave-uniform: softmax offset fixed at 0 (MODE >= 1)
+    // wave-uniform: softmax offset fixed at 0 (MODE >= 1).  FAST0 (bit 32): tile 0 too starts on the
+    // fixed offset, its row sums checked from both sides (2^-64 <= sum <= 2^64: no row can underflow
+    // to l = 0 later); a row outside sends tile 0 to the general path, which sets the exact max
+    bool fast = MODE >= 1 && FAST0;
     const f32x16 zero16 = {};
 
     // O^T += V^T P^T with the V^T fragments read by inline asm (no wait on the LDS-DMA in flight):
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                             pf[kt2][s2][j] = (__bf16)pv_;
                         }
                 psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-                overflow = __any(!(psum <= 0x1p64f));
+                overflow = __any(!(psum <= 0x1p64f)) || (FAST0 && t == 0 && __any(!(psum >= 0x1p-64f)));
             }
             if (!overflow) {
                 if (MODE == 2) {
@@ -473,6 +477,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         switch (v) {
+            case 61: CE_ATTN_LAUNCH(false, 61); break;
             case 29: CE_ATTN_LAUNCH(false, 29); break;
             case 16: CE_ATTN_LAUNCH(false, 16); break;
             case 0: CE_ATTN_LAUNCH(false, 0); break;
@@ -490,7 +495,8 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
-    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29)
+    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
+                  var == 61)
                      ? var : 13;
     return prev;
 }

@@ -278,13 +278,15 @@ int ce_set_gemm_auto(int mode);
  * without a fragment read.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
-/* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key tile
- * on the general online-softmax path: row max, offset accumulators, deferred rescale; 1 = fixed-offset
- * tiles once tile 0's row maxima lie within +-64 log2 units: no row max, no offset, overflow-checked
- * row sums, an overflowing tile redone on the general path; 2 = as 1 with the row sums taken by the
- * MFMA), 4 = one barrier per key tile, 8 = 16-B output stores.  Selectable: 0, 1, 2, 5, 9, 13
- * (default); anything else restores the default.  Causal launches (text tower) use mode 0 with bit 8
- * when set.  Returns the previous variant. */
+/* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key
+ * tile on the general online-softmax path: row max, offset accumulators, deferred rescale; 1 =
+ * fixed-offset tiles once tile 0's row maxima lie within +-64 log2 units: no row max, no offset,
+ * overflow-checked row sums, an overflowing tile redone on the general path; 2 = as 1 with the row
+ * sums taken by the MFMA), 4 = one barrier per key tile, 8 = 16-B output stores, 16 = V^T fragments
+ * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
+ * offset too (row sums checked from both sides).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61; anything
+ * else restores the default.  Causal launches (text tower) use mode 0 with bits 8 and 16 when set.
+ * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
  * register-blocked 96 x 128 kernel (default, for 16-B aligned operands with K % 4 == 0), 0 = the
