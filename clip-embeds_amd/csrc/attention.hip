@@ -46,6 +46,16 @@ __device__ __forceinline__ s16x4 ds_read_tr16_asm(const char* p) {
     return r;
 }
 
+// buffer descriptor from wave-uniform inputs (readfirstlane: no waterfall loops, guide T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_srd(const void* base, int nbytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const int n = __builtin_amdgcn_readfirstlane(nbytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n,
+                                             0x00020000);
+}
+
 __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -70,6 +80,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
     constexpr bool ASMV = (VAR & 16) != 0;   // V^T reads by inline asm (no vmcnt(0) before P.V)
     constexpr bool FAST0 = (VAR & 32) != 0;  // tile 0 on the fixed offset too (two-sided check)
+    constexpr bool BUFDMA = (VAR & 64) != 0; // K/V DMAs through clipped buffer descriptors
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -119,8 +130,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const bf16_t* kbase = base + D + h * 64;
     const bf16_t* vbase = base + 2 * D + h * 64;
 
+    // BUFDMA: the K / V columns of this (b, h) as buffer descriptors clipped after row L - 1 (rows
+    // past the end read zeros: masked keys), per-lane row/chunk offsets computed once, the tile's
+    // row offset one scalar add per DMA (the flat form rebuilt 64-bit addresses with 64-bit
+    // multiplies for every DMA)
+    const int ld2 = (int)ld * 2;
+    const int nrec = BUFDMA ? (L - 1) * ld2 + 128 : 0;
+    const __amdgpu_buffer_rsrc_t ksrd = attn_srd(kbase, nrec);
+    const __amdgpu_buffer_rsrc_t vsrd = attn_srd(vbase, nrec);
+    int kvo[2] = {0, 0}, vvo[2] = {0, 0};
+    if constexpr (BUFDMA) {
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            kvo[ps] = (ps * 32 + srow) * ld2 + kchunk * 16;
+            vvo[ps] = (ps * 32 + srow) * ld2 + vchunk * 16;
+        }
+    }
     auto stage = [&](int t, int buf) {
         char* dst = smem + buf * STAGE_BYTES + wave * 1024;
+        if constexpr (BUFDMA) {
+            const int ro = t * KBLK * ld2;
+#pragma unroll
+            for (int ps = 0; ps < 2; ++ps) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (CE_LDS void*)(dst + ps * 4096), 16, kvo[ps] + ro, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (CE_LDS void*)(dst + TILE_KV_BYTES + ps * 4096), 16,
+                                                         vvo[ps] + ro, 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
             const int key = min(t * KBLK + ps * 32 + srow, L - 1);
@@ -472,11 +509,13 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var;
     if (causal) {
-        if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
+        if ((v & 88) == 88) CE_ATTN_LAUNCH(true, 88);
+        else if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
         else if (v & 8) CE_ATTN_LAUNCH(true, 8);
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         switch (v) {
+            case 125: CE_ATTN_LAUNCH(false, 125); break;
             case 61: CE_ATTN_LAUNCH(false, 61); break;
             case 29: CE_ATTN_LAUNCH(false, 29); break;
             case 16: CE_ATTN_LAUNCH(false, 16); break;
@@ -496,7 +535,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61)
+                  var == 61 || var == 125)
                      ? var : 13;
     return prev;
 }

@@ -284,8 +284,9 @@ int ce_set_gemm_variant(int bits);
  * overflow-checked row sums, an overflowing tile redone on the general path; 2 = as 1 with the row
  * sums taken by the MFMA), 4 = one barrier per key tile, 8 = 16-B output stores, 16 = V^T fragments
  * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
- * offset too (row sums checked from both sides).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61; anything
- * else restores the default.  Causal launches (text tower) use mode 0 with bits 8 and 16 when set.
+ * offset too (row sums checked from both sides), 64 = K/V DMAs through row-clipped buffer descriptors.
+ * Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125; anything
+ * else restores the default.  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
