@@ -171,6 +171,44 @@ __global__ __launch_bounds__(256) void im2col_k(const void* __restrict__ pix, bf
     cols[idx] = f2bf(val);
 }
 
+// Patchify with one wave per patch row for patch 14 (ViT-L/14): lane (c, ky) = (lane / 14, lane % 14),
+// lanes 0..41, moves one 14-pixel run of channel c, image row py * 14 + ky (f32: 7 x 8-B loads;
+// bf16: 7 x 4-B loads) to columns c * 196 + ky * 14 .. + 13 (7 x 4-B stores of bf16 pairs); lanes
+// 42..63 zero the K padding (588 .. Kp - 1, in bf16 pairs).  4 patch rows per 256-thread block.
+template <bool PIX_BF16>
+__global__ __launch_bounds__(256) void im2col14_k(const void* __restrict__ pix, bf16_t* __restrict__ cols, int rows,
+                                                  int S, int Kp) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int G = S / 14;
+    const int b = row / (G * G), pidx = row - b * (G * G);
+    const int py = pidx / G, px = pidx - py * G;
+    uint32_t* out = reinterpret_cast<uint32_t*>(cols + (size_t)row * Kp);
+    if (lane < 42) {
+        const int c = lane / 14, ky = lane - c * 14;
+        const size_t off = (((size_t)b * 3 + c) * S + (size_t)(py * 14 + ky)) * S + px * 14;
+        uint32_t w[7];
+        if constexpr (PIX_BF16) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(static_cast<const bf16_t*>(pix) + off);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) w[k] = src[k];
+        } else {
+            const float2* src = reinterpret_cast<const float2*>(static_cast<const float*>(pix) + off);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const float2 v = src[k];
+                w[k] = pack_bf2(v.x, v.y);
+            }
+        }
+        uint32_t* dst = out + (c * 196 + ky * 14) / 2;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) dst[k] = w[k];
+    } else {
+        for (int q = 294 + (lane - 42); q < Kp / 2; q += 22) out[q] = 0u;
+    }
+}
+
 __global__ __launch_bounds__(256) void cls_rows_k(float* x, const float* cls, const float* pos, int B,
                                                   int Lv, int D) {
     const int b = blockIdx.y;
@@ -413,6 +451,13 @@ hipError_t launch_layernorm(const LNParams& p, bool out_bf16, hipStream_t s) {
 hipError_t launch_im2col(const void* pix, bool pix_bf16, bf16_t* cols, int B, int S, int patch,
                          int Kp, hipStream_t s) {
     const int G = S / patch;
+    if (patch == 14 && Kp % 2 == 0 && Kp >= 588 && S % 2 == 0) {
+        const int rows = B * G * G;
+        const dim3 g4((unsigned)((rows + 3) / 4));
+        if (pix_bf16) hipLaunchKernelGGL(im2col14_k<true>, g4, dim3(256), 0, s, pix, cols, rows, S, Kp);
+        else hipLaunchKernelGGL(im2col14_k<false>, g4, dim3(256), 0, s, pix, cols, rows, S, Kp);
+        return hipGetLastError();
+    }
     const long total = (long)B * G * G * Kp;
     const dim3 grid((unsigned)((total + 255) / 256));
     if (pix_bf16) hipLaunchKernelGGL(im2col_k<true>, grid, dim3(256), 0, s, pix, cols, B, S, patch, Kp);
