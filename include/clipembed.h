@@ -286,7 +286,7 @@ int ce_set_gemm_variant(int bits);
  * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
  * offset too (row sums checked from both sides), 64 = K/V DMAs through row-clipped buffer descriptors.
  * Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125; anything
- * else restores the default.  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
+ * else restores the default (125).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
