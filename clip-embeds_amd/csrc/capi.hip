@@ -436,6 +436,7 @@ struct EpiArgs {
     const float* fold_c = nullptr;
     const bf16_t* rhl = nullptr;     // hi/lo residual planes (EPI_LN_STATS_HL / EPI_HL_F32)
     long hl_plane = 0;
+    bool onetile = false;            // one tile per four-wave workgroup (the text tower's small grids)
 };
 
 int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
@@ -452,6 +453,7 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.part_elems = h->cur_part ? ce::kGemmPartElems : 0;
     p.xb = ea.xb; p.stats_part = ea.stats_part; p.fold_stats = ea.fold_stats; p.fold_c = ea.fold_c;
     p.rhl = ea.rhl; p.hl_plane = ea.hl_plane;
+    p.onetile = ea.onetile ? 1 : 0;
     const double flops = 2.0 * M * N * K;
     // algorithmic bytes: A, W, the residual read (f32 or two bf16 planes: 4 B either way), the output
     // (f32, bf16, or two bf16 planes) and the bf16 copy of EPI_LN_STATS
@@ -561,6 +563,9 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         last_ea.rhl = w.xn;
         last_ea.hl_plane = (long)M * D;
     }
+    // the text tower's small grids run beside the image tower's persistent GEMMs (second stream):
+    // four-wave kernel, one tile per workgroup, so they take CUs a tile at a time
+    fold.onetile = st.onetile = last_ea.onetile = !vis;
     auto finalize = [&] {
         return timed(h, s, vis ? "ln_stats_v" : "ln_stats_t", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
                      [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s); });

@@ -49,6 +49,10 @@ struct GemmParams {
     unsigned long long* trace = nullptr;   // diagnostic timeline, [block][4] (set_gemm_trace)
     int trace_n = 0;
     int variant = 0;                       // kernel-variant bits for A/B (set_gemm_variant)
+    // the caller's request for one tile per four-wave workgroup (grid = tiles): small grids that
+    // run beside another stream's persistent GEMMs (the text tower beside the image tower) take
+    // CUs one tile at a time as they free up (GEMM_VAR_SMALL_ONETILE, default on)
+    int onetile = 0;
 };
 // EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)

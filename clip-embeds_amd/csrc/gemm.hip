@@ -136,10 +136,14 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        // (default 10 + 6)
        GEMM_VAR_W4_SPREAD12 = 1024, GEMM_VAR_W4_SPREAD8 = 2048,
        // the 10 + 6 spread with B3's DMAs in the gaps that carry no fragment read
-       GEMM_VAR_W4_SPREAD_EVEN = 4096 };
+       GEMM_VAR_W4_SPREAD_EVEN = 4096,
+       // honour GemmParams::onetile: the caller's small grids (text tower) on the four-wave kernels
+       // with one tile per workgroup instead of the 8-wave 4-phase kernel
+       GEMM_VAR_SMALL_ONETILE = 8192 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
-    (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD)
+    (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \
+     GEMM_VAR_SMALL_ONETILE)
 #endif
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, bool CHECK_M, int NJ, int RING, int EPI = EPI_PLAIN>
@@ -2496,9 +2500,9 @@ void plan_tail_rhl(GemmParams& p, int nwg, int grid) {
 
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
 // (GEMM_VAR_W4_ONETILE: one workgroup per tile)
-int w4pp_grid(int nwg) {
+int w4pp_grid(int nwg, bool onetile = false) {
     const int need = ((nwg + 7) / 8) * 8;
-    if (gemm_variant() & GEMM_VAR_W4_ONETILE) return need;
+    if (onetile || (gemm_variant() & GEMM_VAR_W4_ONETILE)) return need;
     const int grid = (num_cus() / 8) * 8;
     return grid < need ? grid : need;
 }
@@ -2523,6 +2527,7 @@ int gemm_auto() {
 bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     const int on = gemm_auto();
     if (!on || gemm_sched() != 1) return false;
+    if (p.onetile) return !resid && (act == ACT_NONE || (gemm_variant() & GEMM_VAR_W4_EPI2) != 0);
     // enough tiles that the persistent grid's last-round imbalance stays small (small grids keep
     // SCHED 1 and its split-K tail)
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -2579,14 +2584,14 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         // SCHED 1 (r02 A/B at B = 256: out-proj 682 vs 589 TF/s, c_proj 1,092 vs 995)
         const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
         if ((gemm_variant() & GEMM_VAR_W4_RHL) && gemm_auto() != 0 && gemm_sched() == 1 && p.N % BN == 0 &&
-            p.K >= 2 * BK && nwg >= 2 * num_cus()) {
+            p.K >= 2 * BK && (nwg >= 2 * num_cus() || p.onetile)) {
             p.gm = gemm_groupm();
             p.stagger = gemm_stagger();
-            plan_tail_rhl(p, nwg, w4pp_grid(nwg));
+            plan_tail_rhl(p, nwg, w4pp_grid(nwg, p.onetile));
             const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
             if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
-                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
-            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
             else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
             else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
@@ -2608,7 +2613,7 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         p.gm = gemm_groupm();
         p.stagger = gemm_stagger();
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-        const int grid = w4pp_grid(nwg);
+        const int grid = w4pp_grid(nwg, p.onetile);
         plan_tail_w4(p, nwg, grid);
         if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
             (gemm_variant() & GEMM_VAR_W4_SPREAD12))
@@ -2688,7 +2693,7 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
     } else if (sc == 11) {
         p.stagger = gemm_stagger();
-        const int grid = w4pp_grid(nwg);
+        const int grid = w4pp_grid(nwg, p.onetile);
         plan_tail_w4(p, nwg, grid);
         if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
             (gemm_variant() & GEMM_VAR_W4_SPREAD12))
@@ -2792,6 +2797,7 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     p.trace = g_trace;
     p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
     p.variant = gemm_variant();
+    p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
