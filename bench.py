@@ -304,6 +304,7 @@ def main():
     ap.add_argument("--serial-towers", action="store_true", help="clip: both towers on one stream")
     ap.add_argument("--tower-priority", action="store_true", help="clip: image tower on a high-priority stream")
     ap.add_argument("--attn-var", type=int, default=-1, help="attention forward variant for A/B (-1 = default)")
+    ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM variant bits for A/B (-1 = default)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -322,6 +323,9 @@ def main():
     if args.attn_var >= 0:
         from clipembed import _lib
         _lib.lib().ce_set_attn_variant(args.attn_var)
+    if args.gemm_variant >= 0:
+        from clipembed import _lib
+        _lib.lib().ce_set_gemm_variant(args.gemm_variant)
     t0 = time.time()
     W = BUILDERS[args.workload](args, dev, rank, world)
     engine, step = W["engine"], W["step"]
