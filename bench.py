@@ -128,6 +128,20 @@ def load_traffic(tag):
 
 
 # ----------------------------------------------------------------------------------- workloads
+def pooled_prune_flops(cfg, on=True):
+    """FLOPs per pair NOT executed when pooled-only calls run each tower's last block for the pooled
+    row only (ce_set_pooled_prune): out-proj, c_fc, c_proj and attention for the other rows, counted
+    as the reference's profile counts them (full L x L attention).  Returns (image, text)."""
+    if not on:
+        return 0.0, 0.0
+    v, t = cfg.vision, cfg.text
+    Lv = (v.image_size // v.patch_size) ** 2 + 1
+    img = (Lv - 1) * (2.0 * v.width ** 2 + 4.0 * v.width * v.mlp_width) + 4.0 * v.width * Lv * (Lv - 1)
+    L = cfg.context_length
+    txt = (L - 1) * (2.0 * t.width ** 2 + 4.0 * t.width * t.mlp_width) + 4.0 * t.width * L * (L - 1)
+    return img, txt
+
+
 def build_clip(args, dev, rank, world):
     import clipembed
     from clipembed import _lib, weights as W
@@ -181,7 +195,9 @@ def build_clip(args, dev, rank, world):
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}",
             "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none"}
+    pi, pt = pooled_prune_flops(cfg, not args.no_pooled_prune)
     return dict(engine=model.engine, step=step, pairs=B, flops_per_pair=FLOPS_PER_PAIR, sd=sd, cfg=cfg,
+                flops_exec_per_pair=FLOPS_PER_PAIR - pi - pt,
                 metric="image-text pairs/sec ViT-L/14-336", config=cfgd)
 
 
@@ -216,8 +232,10 @@ def build_pacl(args, dev, rank, world):
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}", "pacl_mode": args.pacl_mode,
             "exchange": "RCCL all_gather of pooled embeddings" if world > 1 else "none"}
+    _, pt = pooled_prune_flops(cfg, not args.no_pooled_prune)    # the PACL text tower is pooled-only
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
                 flops_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops,
+                flops_exec_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops - pt,
                 metric="PACL image-text pairs/sec ViT-L/14-336", config=cfgd, hbm_kernel="pacl_pool")
 
 
@@ -247,7 +265,9 @@ def build_negclip(args, dev, rank, world):
             "batch_per_gpu": B, "hard_negatives_per_gpu": K, "global_batch": world * B, "parallelism": f"dp{world}",
             "exchange": ("RCCL all_gather of embeddings + sizes, reduce_scatter of their gradients, "
                          "all_reduce of text gradients") if world > 1 else "none"}
+    pi, _ = pooled_prune_flops(cfg, not args.no_pooled_prune)     # locked image tower: pooled-only
     return dict(engine=m.engine, step=step, pairs=B, flops_per_pair=flops, sd=sd, cfg=cfg,
+                flops_exec_per_pair=flops - pi,
                 metric="NegCLIP training image-text pairs/sec ViT-L/14-336", config=cfgd)
 
 
@@ -305,6 +325,10 @@ def main():
     ap.add_argument("--tower-priority", action="store_true", help="clip: image tower on a high-priority stream")
     ap.add_argument("--attn-var", type=int, default=-1, help="attention forward variant for A/B (-1 = default)")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM variant bits for A/B (-1 = default)")
+    ap.add_argument("--no-pooled-prune", action="store_true",
+                    help="run every tower's last block for all rows (A/B of ce_set_pooled_prune)")
+    ap.add_argument("--gemm-stagger", type=int, default=-1,
+                    help="first-round stagger of the persistent residual GEMMs (x s_sleep 127, odd slots; A/B)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -326,6 +350,13 @@ def main():
     if args.gemm_variant >= 0:
         from clipembed import _lib
         _lib.lib().ce_set_gemm_variant(args.gemm_variant)
+    if args.no_pooled_prune:
+        os.environ["CE_POOLED_PRUNE"] = "0"          # read at ce_create
+    if args.gemm_stagger >= 0:
+        from clipembed import _lib
+        L = _lib.lib()
+        prev = L.ce_set_gemm_schedule(1)
+        L.ce_set_gemm_schedule((prev & 0xffff) | ((args.gemm_stagger + 1) << 24))
     t0 = time.time()
     W = BUILDERS[args.workload](args, dev, rank, world)
     engine, step = W["engine"], W["step"]
@@ -397,7 +428,11 @@ def main():
             ach = (top["bytes"] / top["launches"]) / (per_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": load_traffic(top["name"])}
-        roof["step_mfma_frac"] = round(value * W["flops_per_pair"] / 1e12 / world / PEAK_BF16_TFLOPS, 4)
+        # executed FLOPs (the pooled-only prune skips part of the last blocks) and the reference
+        # model's FLOPs per pair (open_clip's profile), both over the dense bf16 peak
+        fx = W.get("flops_exec_per_pair", W["flops_per_pair"])
+        roof["step_mfma_frac"] = round(value * fx / 1e12 / world / PEAK_BF16_TFLOPS, 4)
+        roof["model_flops_frac"] = round(value * W["flops_per_pair"] / 1e12 / world / PEAK_BF16_TFLOPS, 4)
         hk = W.get("hbm_kernel")
         if hk:
             hs = [s for s in profile if s["name"] == hk]

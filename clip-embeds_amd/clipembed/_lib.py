@@ -105,6 +105,7 @@ _SIGNATURES = {
     "ce_set_gemm_splitk": (c_int, [c_int]),
     "ce_set_ln_fold": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "ce_set_resid_hl": (c_int, [c_void_p, c_int, POINTER(c_int)]),
+    "ce_set_pooled_prune": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "ce_kernel_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int]),
     "ce_kernel_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int]),
     "ce_train_bind": (c_int, [c_void_p, POINTER(Tensor), POINTER(Tensor), c_int]),

@@ -112,6 +112,13 @@ class Engine:
         _lib.call("ce_set_resid_hl", self.h, 1 if on else 0, ctypes.byref(prev))
         return prev.value == 1
 
+    def set_pooled_prune(self, on: bool) -> bool:
+        """Run each tower's last block for the pooled rows only (CLS / EOT) when no tokens are
+        requested (default on); returns the previous setting (ce_set_pooled_prune)."""
+        prev = ctypes.c_int()
+        _lib.call("ce_set_pooled_prune", self.h, 1 if on else 0, ctypes.byref(prev))
+        return prev.value == 1
+
     # ---- timing (roofline reporting) ----
     def set_timing(self, on: bool, only: str = ""):
         """Bracket kernel launches with HIP events (all tags, or only the launches tagged `only`)."""

@@ -498,7 +498,98 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 
 int g_attn_var = 125;
 
+// One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
+// mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
+// of the image tower, the EOT row qrows[b] of the text tower).  Workgroup =
+// (head, batch), 256 threads: scores with one key per thread (the row's 128 B as eight 16-B
+// loads), block max / sum, then P.V with 16 key slots x 16 four-column groups and a fixed-order
+// slot sum.  Same arithmetic as attn_fwd where it matters: q arrives pre-scaled by log2(e)/8 (the
+// engine's in_proj weights), scores in log2 units, p = exp2(s - max); P stays f32 here.
+// Optionally copies the selected row's 64 columns of the hi/lo residual planes to compact planes
+// (the residual of the pruned out-projection).
+__global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qkv, const int* __restrict__ qrows,
+                                                   int L, int H, int causal, bf16_t* __restrict__ out,
+                                                   const bf16_t* __restrict__ src, long splane,
+                                                   bf16_t* __restrict__ dst, long dplane) {
+    extern __shared__ float sc[];                 // [L]: scores, then probabilities
+    __shared__ float qs[64];
+    __shared__ float red[2][4];
+    __shared__ float pv[16][68];
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int D = H * 64;
+    const long ld = 3L * D;
+    const long row0 = (long)b * L;
+    const long qr = qrows ? (long)qrows[b] : row0;
+    const int nk = causal ? (int)(qr - row0) + 1 : L;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t < 64) qs[t] = bf2f(qkv[qr * ld + h * 64 + t]);
+    if (src && t < 128) {
+        const int pl = t >> 6;
+        dst[pl * dplane + (long)b * D + h * 64 + lane] = src[pl * splane + qr * D + h * 64 + lane];
+    }
+    __syncthreads();
+    float m = -INFINITY;
+    for (int j = t; j < nk; j += 256) {
+        const uint4* kp = reinterpret_cast<const uint4*>(qkv + (row0 + j) * ld + D + h * 64);
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint4 u = kp[c];
+            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s = fmaf(qs[c * 8 + 2 * e], __uint_as_float(w[e] << 16), s);
+                s = fmaf(qs[c * 8 + 2 * e + 1], __uint_as_float(w[e] & 0xffff0000u), s);
+            }
+        }
+        sc[j] = s;
+        m = fmaxf(m, s);
+    }
+    m = wave_max(m);
+    if (lane == 0) red[0][wave] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float l = 0.f;
+    for (int j = t; j < nk; j += 256) {
+        const float p = exp2f(sc[j] - m);
+        sc[j] = p;
+        l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) red[1][wave] = l;
+    __syncthreads();
+    l = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    const int ks = t >> 4, d0 = (t & 15) * 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    const bf16_t* vb = qkv + row0 * ld + 2 * D + h * 64 + d0;
+    for (int j = ks; j < nk; j += 16) {
+        const uint2 v = *reinterpret_cast<const uint2*>(vb + j * ld);
+        const float p = sc[j];
+        a0 = fmaf(p, __uint_as_float(v.x << 16), a0);
+        a1 = fmaf(p, __uint_as_float(v.x & 0xffff0000u), a1);
+        a2 = fmaf(p, __uint_as_float(v.y << 16), a2);
+        a3 = fmaf(p, __uint_as_float(v.y & 0xffff0000u), a3);
+    }
+    pv[ks][d0] = a0; pv[ks][d0 + 1] = a1; pv[ks][d0 + 2] = a2; pv[ks][d0 + 3] = a3;
+    __syncthreads();
+    if (t < 64) {
+        float o = 0.f;
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) o += pv[k2][t];
+        out[(long)b * D + h * 64 + t] = f2bf(o / l);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
+                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s) {
+    if (B <= 0 || L <= 0) return hipSuccess;
+    if ((size_t)L * 4 > 96 * 1024 || B > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(attn_rows_k, dim3(H, B), dim3(256), (size_t)L * 4, s, qkv, qrows, L, H, causal ? 1 : 0, out,
+                       src, splane, dst, dplane);
+    return hipGetLastError();
+}
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse) {

@@ -161,6 +161,9 @@ struct ce_handle {
     // folded image tower: residual stream inside the blocks as hi/lo bf16 planes (EPI_LN_STATS_HL;
     // env CE_RESID_HL=0 keeps the f32 stream + bf16 copy)
     bool resid_hl = true;
+    // pooled-only calls (no tokens requested): the last block of each tower runs for the pooled
+    // rows only (CLS / EOT); env CE_POOLED_PRUNE=0 / ce_set_pooled_prune(h, 0)
+    bool pooled_prune = true;
     std::map<std::string, bool> folded;
     // text-tower training: caller-owned f32 master values and gradient slots per
     // trainable tensor (device pointers), saved activations of the last ce_text_forward_train
@@ -597,9 +600,63 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     return CE_OK;
 }
 
+// The last folded block of a tower when only its pooled rows are consumed (pooled-only
+// encode_image / encode_text): row sel[b] of sequence b (null: b * L, the CLS row).  The QKV GEMM
+// still covers every row (keys and values of the whole sequence); attention runs for the selected
+// query rows only, and out-proj, c_fc and c_proj for those B rows — the other rows' outputs of
+// this block feed nothing (the reference pools x[:, 0] / x[arange, argmax] after ln_post /
+// ln_final, transformer.py:718-741, model.py:295-299).  Leaves the selected rows' final f32 x
+// compact in w.x [B][D].  Compact work buffers: attention rows, then the residual hi/lo planes, in
+// w.att; LN statistics of the B rows in w.stats / w.stats_part; c_fc output in w.hid.
+int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, const FoldBlk& f, int B, int L,
+                     int D, int H, int F, const int* sel, bool vis) {
+    const int M = B * L;
+    struct PartScope {
+        ce_handle* h;
+        ~PartScope() { h->cur_part = nullptr; }
+    } scope{h};
+    h->cur_part = w.part;
+    EpiArgs fold;
+    fold.epi = ce::EPI_LN_FOLD;
+    fold.fold_stats = w.stats;
+    fold.onetile = !vis;
+    fold.fold_c = f.cqkv;
+    CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
+                nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
+    bf16_t* att = w.att;                          // [B][D]
+    bf16_t* xc = w.att + (size_t)B * D;           // hi plane [B][D], lo plane after it
+    const long cplane = (long)B * D;
+    {
+        const double flops = 4.0 * B * H * (double)L * 64;
+        const double bytes = (double)M * 2 * D * 2 + (double)B * D * 2 * 4;
+        CE_TRY(timed(h, s, vis ? "attn_pool_v" : "attn_pool_t", flops, bytes, [&] {
+            return ce::launch_attention_rows(w.qkv, sel, att, B, L, H, !vis, w.xn, (long)M * D, xc, cplane, s);
+        }));
+    }
+    EpiArgs st;
+    st.epi = ce::EPI_LN_STATS_HL;
+    st.xb = xc;
+    st.stats_part = w.stats_part;
+    st.rhl = xc;
+    st.hl_plane = cplane;
+    CE_TRY(gemm(h, s, vis ? "gemm_out_pool_v" : "gemm_out_pool_t", att, D, k.wout, B, D, D, k.bout, ce::ACT_NONE_, nullptr,
+                w.x, false, 0, 0, 0, 0, 0, st));
+    CE_TRY(timed(h, s, vis ? "ln_stats_pool_v" : "ln_stats_pool_t", 0.0, (double)B * (D / 64) * 8 + (double)B * 8,
+                 [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, B, D / 64, s); }));
+    fold.fold_c = f.cfc;
+    CE_TRY(gemm(h, s, vis ? "gemm_fc_pool_v" : "gemm_fc_pool_t", xc, D, f.wfc, B, F, D, f.dfc, act_code(h), nullptr, w.hid,
+                true, 0, 0, 0, 0, 0, fold));
+    EpiArgs last_ea;
+    last_ea.epi = ce::EPI_HL_F32;
+    last_ea.rhl = xc;
+    last_ea.hl_plane = cplane;
+    return gemm(h, s, vis ? "gemm_proj_pool_v" : "gemm_proj_pool_t", w.hid, F, k.wproj, B, D, F, k.bproj, ce::ACT_NONE_,
+                nullptr, w.x, false, 0, 0, 0, 0, 0, last_ea);
+}
+
 // Vision tower.  Leaves the final residual stream in w.x.  out_pooled may be null.
 int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, bool pix_bf16, int B,
-               float* out_pooled, bool normalize) {
+               float* out_pooled, bool normalize, bool keep_tokens = true) {
     const ce_config& c = h->cfg;
     const int D = c.vision.width, G = h->G, P = G * G, Lv = P + 1;
     // _embeds: conv1 as a patch GEMM whose epilogue scatters row (b,p) to b*Lv+1+p and adds pos[1+p]
@@ -628,16 +685,21 @@ int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, b
         CE_TRY(layernorm(h, s, "ln_v", w.x, w.x, false, W(h, "visual.ln_pre.weight"), W(h, "visual.ln_pre.bias"),
                          B * Lv, D));
     }
+    // pooled rows only (no tokens wanted): the last block for the CLS rows alone
+    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && Lv >= 3;
     for (int i = 0; i < c.vision.layers; ++i) {
         const Blk k = block_ptrs(h, "visual.transformer.resblocks." + std::to_string(i) + ".");
-        if (use_fold)
-            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, Lv, D, c.vision.heads, c.vision.mlp_width,
-                                    i + 1 == c.vision.layers));
+        const bool last = i + 1 == c.vision.layers;
+        if (prune && last)
+            CE_TRY(run_block_pooled(h, s, w, k, folds[i], B, Lv, D, c.vision.heads, c.vision.mlp_width, nullptr,
+                                    true));
+        else if (use_fold)
+            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, Lv, D, c.vision.heads, c.vision.mlp_width, last));
         else
             CE_TRY(run_block(h, s, w, k, B, Lv, D, c.vision.heads, c.vision.mlp_width, false, true));
     }
     if (out_pooled) {
-        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, nullptr, (long)Lv * D, B, D,
+        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, nullptr, prune ? (long)D : (long)Lv * D, B, D,
                                                  W(h, "visual.ln_post.weight"), W(h, "visual.ln_post.bias"), s),
                             "ln_post(pool)"));
         ce::FGemmParams fp{};
@@ -651,7 +713,7 @@ int run_vision(ce_handle* h, hipStream_t s, const TowerWs& w, const void* pix, b
 }
 
 int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, int B, float* out_pooled,
-             bool normalize) {
+             bool normalize, bool keep_tokens = true) {
     const ce_config& c = h->cfg;
     const int D = c.text.width, L = c.context_length;
     // LN folding as in the image tower: every block's fold current, D a multiple of 64
@@ -670,17 +732,21 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
                                                   W(h, "positional_embedding"), B, L, D, c.vocab_size, s),
                             "token_embedding"));
     }
+    // pooled rows only (no tokens wanted): the last block for the EOT rows alone
+    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && L >= 3;
+    if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     for (int i = 0; i < c.text.layers; ++i) {
         const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(i) + ".");
-        if (use_fold)
-            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width,
-                                    i + 1 == c.text.layers, false));
+        const bool last = i + 1 == c.text.layers;
+        if (prune && last)
+            CE_TRY(run_block_pooled(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, w.rows, false));
+        else if (use_fold)
+            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, last, false));
         else
             CE_TRY(run_block(h, s, w, k, B, L, D, c.text.heads, c.text.mlp_width, true, false));
     }
     if (out_pooled) {
-        CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
-        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, w.rows, D, B, D, W(h, "ln_final.weight"),
+        CE_TRY(check_launch(ce::launch_ln_gather(w.pooled, w.x, prune ? nullptr : w.rows, D, B, D, W(h, "ln_final.weight"),
                                                  W(h, "ln_final.bias"), s), "ln_final(pool)"));
         ce::FGemmParams fp{};
         fp.A = w.pooled; fp.lda = D; fp.B = W(h, "text_projection"); fp.ldb = c.embed_dim;
@@ -977,6 +1043,7 @@ int ce_create(const ce_config* cfg, int device, ce_handle** out) {
     ce_handle* h = new ce_handle();
     if (const char* e = getenv("CE_LN_FOLD")) h->ln_fold = atoi(e) != 0;
     if (const char* e = getenv("CE_RESID_HL")) h->resid_hl = atoi(e) != 0;
+    if (const char* e = getenv("CE_POOLED_PRUNE")) h->pooled_prune = atoi(e) != 0;
     h->cfg = *cfg;
     h->device = device;
     h->G = cfg->image_size / cfg->patch_size;
@@ -1235,7 +1302,7 @@ int ce_encode_image(ce_handle* h, void* stream, const void* pixels, int pixel_dt
     const long P = (long)h->G * h->G, Lv = P + 1;
     const int D = h->cfg.vision.width;
     TowerWs w = carve(h->ws, B * Lv, D, h->cfg.vision.mlp_width, B * P * h->Kp, B);
-    CE_TRY(run_vision(h, s, w, pixels, pixel_dtype == CE_BF16, B, out_pooled, normalize != 0));
+    CE_TRY(run_vision(h, s, w, pixels, pixel_dtype == CE_BF16, B, out_pooled, normalize != 0, out_tokens != nullptr));
     if (out_tokens)
         CE_TRY(layernorm(h, s, "ln_v", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "visual.ln_post.weight"),
                          W(h, "visual.ln_post.bias"), (int)(B * P), D, (int)P, (int)Lv, 1, (int)P, 0));
@@ -1257,7 +1324,7 @@ int ce_encode_text(ce_handle* h, void* stream, const int64_t* ids, int B, int ct
     CE_TRY(ensure_ws_text(h, text_bytes(h, B)));
     const int D = h->cfg.text.width;
     TowerWs w = carve(h->ws_t, (long)B * ctx, D, h->cfg.text.mlp_width, 0, B);
-    CE_TRY(run_text(h, s, w, ids, B, out_pooled, normalize != 0));
+    CE_TRY(run_text(h, s, w, ids, B, out_pooled, normalize != 0, out_tokens != nullptr));
     if (out_tokens)
         CE_TRY(layernorm(h, s, "ln_final_t", w.x, out_tokens, tokens_dtype == CE_BF16, W(h, "ln_final.weight"),
                          W(h, "ln_final.bias"), B * ctx, D));
@@ -1418,7 +1485,7 @@ int ce_pacl_forward(ce_handle* h, void* stream, const void* pixels, int pixel_dt
     // 1) text tower + PACL text head (pacl.py:116-118)
     {
         TowerWs w = carve(h->ws, (long)Bt * c.context_length, c.text.width, c.text.mlp_width, 0, Bt);
-        CE_TRY(run_text(h, s, w, ids, Bt, tclip, false));
+        CE_TRY(run_text(h, s, w, ids, Bt, tclip, false, false));
         float* ln = (float*)h->tmp + 0;
         ln = (float*)(h->tmp + align256((size_t)Bt * E * 4) + align256((size_t)Bt * Pd * 4));
         CE_TRY(check_launch(ce::launch_ln_gather(ln, tclip, nullptr, E, Bt, E, W(h, "text_projection.0.weight"),
@@ -1901,6 +1968,13 @@ int ce_set_resid_hl(ce_handle* h, int enable, int* previous) {
     if (!h) return fail(CE_ERR_INVALID, "ce_set_resid_hl: null handle");
     if (previous) *previous = h->resid_hl ? 1 : 0;
     h->resid_hl = enable != 0;
+    return CE_OK;
+}
+
+int ce_set_pooled_prune(ce_handle* h, int enable, int* previous) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_set_pooled_prune: null handle");
+    if (previous) *previous = h->pooled_prune ? 1 : 0;
+    h->pooled_prune = enable != 0;
     return CE_OK;
 }
 

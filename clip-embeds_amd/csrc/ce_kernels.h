@@ -83,6 +83,12 @@ int set_attn_variant(int var);  // attention forward variant (0-2) for A/B; retu
 int set_fgemm_variant(int v);   // 1 = register-blocked f32 GEMM (default), 0 = the 64 x 64 kernel
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse = nullptr);   // lse: [B][H][L] log2 log-sum-exp (training)
+// The same attention for ONE query row per sequence (row qrows[b], absolute; null: row b*L), keys
+// of sequence b only (0..qrows[b]-b*L with causal); out [B][D] bf16 compact.  q pre-scaled as
+// launch_attention(q_prescaled).  src/dst (optional): copy the selected rows of the hi/lo planes
+// (plane strides splane / dplane elements) to compact rows b of dst.
+hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
+                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s);
 
 // LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.
 //   in row  = (r / grp) * i_gs + i_go + r % grp   (grp == 0: identity)

@@ -334,6 +334,12 @@ int ce_set_ln_fold(ce_handle* h, int enable, int* previous);
  * copy: 4 B per element written instead of 6; |x - (hi + lo)| <= 2^-16 |x|.  The tower's last
  * residual GEMM writes f32 x.  *previous (may be null) gets the previous setting. */
 int ce_set_resid_hl(ce_handle* h, int enable, int* previous);
+/* Pooled-only encode calls (out_tokens null; the PACL text tower) run each tower's last block for
+ * the pooled rows only — the CLS row of every image, the EOT (argmax id) row of every caption —
+ * since no other row of that block reaches the output (transformer.py:718-741, model.py:295-299).
+ * Default on with the LN-folded hi/lo towers (env CE_POOLED_PRUNE=0 at ce_create turns it off);
+ * *previous (may be null) gets the previous setting. */
+int ce_set_pooled_prune(ce_handle* h, int enable, int* previous);
 /* Attention core over packed qkv [B*L, 3*H*64] bf16 -> out [B*L, H*64] bf16 (transformer.py:242-255). */
 int ce_kernel_attention(void* stream, const void* qkv, void* out, int B, int L, int H, int causal);
 /* LayerNorm rows [rows, D] f32 -> f32/bf16 (eps 1e-5; transformer.py:23-29).  D % 256 == 0. */

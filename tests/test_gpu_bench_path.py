@@ -214,6 +214,38 @@ def test_batch256_full_depth_bench_path(full_model, golden):
         m.visual.output_tokens = False
 
 
+def test_batch256_pooled_prune(full_model, golden):
+    """The bench's own calls (pooled features only): each tower's last block runs for the pooled
+    rows alone (CLS / EOT; ce_set_pooled_prune).  Asserts the paths (23 c_fc on SCHED 11, the
+    pruned B-row c_fc / out-proj on SCHED 1) and checks the pooled outputs against the unpruned
+    path (2e-5 cosine: the pruned attention keeps P in f32, the small GEMMs sum in another order)
+    and the golden rows against the reference (1e-3)."""
+    m = full_model
+    g, imgs, caps = _bench_batch(golden)
+    assert not m.visual.output_tokens and not m.output_text_tokens
+    path_counts()
+    pi = m.encode_image(imgs)
+    torch.cuda.synchronize()
+    cnt = path_counts()
+    assert cnt[W4PP + FOLD] == 47 and cnt[NT + FOLD] == 1, cnt
+    assert cnt[W4PP + STATS] == 46 and cnt[NT + STATS] == 1 and cnt[FIXUP + STATS] == 46, cnt
+    pt = m.encode_text(caps)
+    prev = m.engine.set_pooled_prune(False)
+    try:
+        assert prev
+        qi = m.encode_image(imgs)
+        qt = m.encode_text(caps)
+    finally:
+        m.engine.set_pooled_prune(prev)
+    pi_n, pt_n = pi.cpu().numpy(), pt.cpu().numpy()
+    d_img, d_txt = cos_dist(pi_n, qi.cpu().numpy()), cos_dist(pt_n, qt.cpu().numpy())
+    print(f"pruned vs full: image {d_img:.3g} text {d_txt:.3g}")
+    assert d_img < 2e-5 and d_txt < 2e-5
+    sel = [0, 255]
+    assert cos_dist(pi_n[sel], g["image_pooled"]) < COS_TOL
+    assert cos_dist(pt_n[sel], g["text_pooled"]) < COS_TOL
+
+
 @pytest.mark.parametrize("tag", ["pacl", "pacl_rope_after"])
 def test_pacl_batch512_golden_rows(golden, tag):
     """PACL forward at the C3 batch (512 pairs, BASELINE configs[2]) with the two golden pairs of

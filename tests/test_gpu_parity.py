@@ -83,6 +83,43 @@ def test_reduced_depth_vs_oracle_batch(small):
     assert cos_dist(pt, O.encode_text(sd, caps, cfg)) < COS_TOL
 
 
+def test_pooled_prune_vs_oracle_ragged(small):
+    """Pooled-only calls run each tower's last block for the pooled rows only (CLS / EOT,
+    ce_set_pooled_prune, default on): against the oracle on 3 images and 5 captions whose EOT sits
+    at positions 1, 76 and in between, and against the unpruned path (prune off, and the tokens
+    call, which never prunes) within 2e-5 cosine."""
+    cfg = small.cfg
+    sd = W.synthetic_state_dict(cfg)
+    imgs = torch.from_numpy(W.synthetic_images(3, seed=77))
+    caps = W.synthetic_captions(5, seed=78)
+    rng = np.random.default_rng(79)
+    caps[0] = 0
+    caps[0, :2] = [49406, 49407]                                  # empty caption: EOT at 1
+    caps[1] = rng.integers(1, 49000, 77)
+    caps[1, 0], caps[1, 76] = 49406, 49407                        # EOT at the last position
+    ct = torch.from_numpy(caps)
+    pi, pt = small.encode_image(imgs), small.encode_text(ct)
+    prev = small.engine.set_pooled_prune(False)
+    try:
+        assert prev
+        qi, qt = small.encode_image(imgs), small.encode_text(ct)
+    finally:
+        small.engine.set_pooled_prune(prev)
+    small.visual.output_tokens = True
+    small.output_text_tokens = True
+    try:
+        ri, _ = small.encode_image(imgs)
+        rt, _ = small.encode_text(ct)
+    finally:
+        small.visual.output_tokens = False
+        small.output_text_tokens = False
+    pi, pt, qi, qt, ri, rt = (x.cpu().numpy() for x in (pi, pt, qi, qt, ri, rt))
+    assert cos_dist(pi, qi) < 2e-5 and cos_dist(pt, qt) < 2e-5
+    assert np.array_equal(qi, ri) and np.array_equal(qt, rt)
+    assert cos_dist(pi, O.encode_image(sd, imgs.numpy(), cfg)) < COS_TOL
+    assert cos_dist(pt, O.encode_text(sd, caps, cfg)) < COS_TOL
+
+
 def test_bf16_pixels(small):
     imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
     a = small.encode_image(imgs)
