@@ -128,18 +128,26 @@ def load_traffic(tag):
 
 
 # ----------------------------------------------------------------------------------- workloads
-def pooled_prune_flops(cfg, on=True):
-    """FLOPs per pair NOT executed when pooled-only calls run each tower's last block for the pooled
-    row only (ce_set_pooled_prune): out-proj, c_fc, c_proj and attention for the other rows, counted
-    as the reference's profile counts them (full L x L attention).  Returns (image, text)."""
+def pooled_prune_flops(cfg, on=True, eot=None):
+    """FLOPs per pair NOT executed by pooled-only calls (ce_set_pooled_prune): the image tower's last
+    block runs out-proj, c_fc, c_proj and attention for the CLS row only; the text tower runs on the
+    rows 0..EOT of each caption (packed; no later row reaches the EOT row under the causal mask) and
+    its last block for the EOT row only.  Counted as the reference's profile counts a forward (full
+    L x L attention; TEXT_FLOPS scaled by this model of the text work).  eot: EOT positions of the
+    captions (None: text not pruned).  Returns (image, text) per pair."""
     if not on:
         return 0.0, 0.0
     v, t = cfg.vision, cfg.text
     Lv = (v.image_size // v.patch_size) ** 2 + 1
     img = (Lv - 1) * (2.0 * v.width ** 2 + 4.0 * v.width * v.mlp_width) + 4.0 * v.width * Lv * (Lv - 1)
-    L = cfg.context_length
-    txt = (L - 1) * (2.0 * t.width ** 2 + 4.0 * t.width * t.mlp_width) + 4.0 * t.width * L * (L - 1)
-    return img, txt
+    if eot is None:
+        return img, 0.0
+    L, D, F, nl = t.context_length, t.width, t.mlp_width, t.layers
+    g = 2.0 * (4 * D * D + 2 * D * F)                        # GEMM FLOPs per row per block
+    full = nl * (L * g + 4.0 * D * L * L)
+    n = np.asarray(eot, np.float64) + 1.0
+    run = (nl - 1) * (n * g + 4.0 * D * n * n) + (n * 6.0 * D * D + 4.0 * D * n + 2.0 * D * D + 4.0 * D * F)
+    return img, TEXT_FLOPS * float(1.0 - run.mean() / full)
 
 
 def build_clip(args, dev, rank, world):
@@ -195,7 +203,7 @@ def build_clip(args, dev, rank, world):
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}",
             "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none"}
-    pi, pt = pooled_prune_flops(cfg, not args.no_pooled_prune)
+    pi, pt = pooled_prune_flops(cfg, not args.no_pooled_prune, caps.cpu().numpy().argmax(1))
     return dict(engine=model.engine, step=step, pairs=B, flops_per_pair=FLOPS_PER_PAIR, sd=sd, cfg=cfg,
                 flops_exec_per_pair=FLOPS_PER_PAIR - pi - pt,
                 metric="image-text pairs/sec ViT-L/14-336", config=cfgd)
@@ -232,7 +240,7 @@ def build_pacl(args, dev, rank, world):
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}", "pacl_mode": args.pacl_mode,
             "exchange": "RCCL all_gather of pooled embeddings" if world > 1 else "none"}
-    _, pt = pooled_prune_flops(cfg, not args.no_pooled_prune)    # the PACL text tower is pooled-only
+    _, pt = pooled_prune_flops(cfg, not args.no_pooled_prune, caps.cpu().numpy().argmax(1))  # pooled-only text
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
                 flops_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops,
                 flops_exec_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops - pt,

@@ -72,8 +72,9 @@ __device__ __forceinline__ void barrier() {
 // the overflow check on a max3 reduction of the scores.
 template <bool CAUSAL, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
-                                                    bf16_t* __restrict__ out, int L, int H,
-                                                    float qscale, float* __restrict__ lse) {
+                                                    bf16_t* __restrict__ out, int Lp, int H,
+                                                    float qscale, float* __restrict__ lse,
+                                                    const int* __restrict__ seg) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
     constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
-    const int nqb = (L + QBLK - 1) / QBLK;
+    const int nqb = (Lp + QBLK - 1) / QBLK;
     const int nwg = gridDim.x;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
@@ -94,7 +95,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int b = bh / H, h = bh - b * H;
     const int D = H * 64;
     const long ld = 3L * D;
-    const bf16_t* base = qkv + (size_t)b * L * ld;
+    // packed sequences (seg: the text tower's pooled-only rows, launch_text_pack): sequence b is
+    // rows seg[b] .. seg[b + 1] - 1; q-blocks past its end exit
+    int L = Lp;
+    long row0 = (long)b * Lp;
+    if (seg) {
+        row0 = seg[b];
+        L = seg[b + 1] - seg[b];
+        if (qb * QBLK >= L) return;
+    }
+    const bf16_t* base = qkv + (size_t)row0 * ld;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -462,8 +472,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (MODE == 2 ? lm[0] : 0.f);
     const float inv = 1.0f / l_tot;
     // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
-    if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * L + qrow] = m_run + __log2f(l_tot);
-    bf16_t* op = out + ((size_t)b * L + min(qrow, L - 1)) * D + h * 64;
+    if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * Lp + qrow] = m_run + __log2f(l_tot);
+    bf16_t* op = out + ((size_t)row0 + min(qrow, L - 1)) * D + h * 64;
     if (WIDE) {
         // lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
         // trades the lower lane's odd-g words for the upper lane's even-g words, so each lane
@@ -510,7 +520,7 @@ int g_attn_var = 125;
 __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qkv, const int* __restrict__ qrows,
                                                    int L, int H, int causal, bf16_t* __restrict__ out,
                                                    const bf16_t* __restrict__ src, long splane,
-                                                   bf16_t* __restrict__ dst, long dplane) {
+                                                   bf16_t* __restrict__ dst, long dplane, const int* __restrict__ seg) {
     extern __shared__ float sc[];                 // [L]: scores, then probabilities
     __shared__ float qs[64];
     __shared__ float red[2][4];
@@ -518,7 +528,7 @@ __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qk
     const int h = blockIdx.x, b = blockIdx.y;
     const int D = H * 64;
     const long ld = 3L * D;
-    const long row0 = (long)b * L;
+    const long row0 = seg ? (long)seg[b] : (long)b * L;
     const long qr = qrows ? (long)qrows[b] : row0;
     const int nk = causal ? (int)(qr - row0) + 1 : L;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -583,20 +593,22 @@ __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qk
 }  // namespace
 
 hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
-                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s) {
+                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s,
+                                 const int* seg) {
     if (B <= 0 || L <= 0) return hipSuccess;
     if ((size_t)L * 4 > 96 * 1024 || B > 65535) return hipErrorInvalidValue;
+    if (seg && (!qrows || !causal)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(attn_rows_k, dim3(H, B), dim3(256), (size_t)L * 4, s, qkv, qrows, L, H, causal ? 1 : 0, out,
-                       src, splane, dst, dplane);
+                       src, splane, dst, dplane, seg);
     return hipGetLastError();
 }
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s, float* lse) {
+                            hipStream_t s, float* lse, const int* seg) {
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
-#define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse)
+#define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var;
     if (causal) {

@@ -350,6 +350,7 @@ struct TowerWs {
     bf16_t* xlo;          // lo plane right after xn (hi/lo residual stream: plane stride rows * D)
     float* pooled;
     int* rows;
+    int* seg;             // packed text rows (pooled-only calls): [B + 1] offsets, seg[B] = live rows
     float* part;     // GEMM split-K partial tiles (ce::kGemmPartElems f32), per tower: the towers may
                      // run concurrently on two streams
     float2* stats;        // LN folding: (mu, rstd) per row of the residual stream
@@ -364,7 +365,7 @@ size_t tower_bytes(long rows, int D, int F, long extra_hid_elems, long B) {
     n += align256(rows * D * 2);
     n += align256(std::max(rows * F, extra_hid_elems) * 2);
     n += align256(B * D * 4);
-    n += align256(B * 4);
+    n += align256((2 * B + 1) * 4);
     n += align256(ce::kGemmPartElems * 4);
     n += align256(rows * 8);
     n += align256(rows * (D / 64) * 8);
@@ -382,7 +383,9 @@ TowerWs carve(char* base, long rows, int D, int F, long extra_hid_elems, long B)
     w.att = (bf16_t*)p; p += align256(rows * D * 2);
     w.hid = (bf16_t*)p; p += align256(std::max(rows * F, extra_hid_elems) * 2);
     w.pooled = (float*)p; p += align256(B * D * 4);
-    w.rows = (int*)p; p += align256(B * 4);
+    w.rows = (int*)p;
+    w.seg = w.rows + B;
+    p += align256((2 * B + 1) * 4);
     w.part = (float*)p; p += align256(ce::kGemmPartElems * 4);
     w.stats = (float2*)p; p += align256(rows * 8);
     w.stats_part = (float2*)p;
@@ -440,6 +443,7 @@ struct EpiArgs {
     const bf16_t* rhl = nullptr;     // hi/lo residual planes (EPI_LN_STATS_HL / EPI_HL_F32)
     long hl_plane = 0;
     bool onetile = false;            // one tile per four-wave workgroup (the text tower's small grids)
+    const int* m_dev = nullptr;      // packed rows: live row count on the device
 };
 
 int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
@@ -457,6 +461,7 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.xb = ea.xb; p.stats_part = ea.stats_part; p.fold_stats = ea.fold_stats; p.fold_c = ea.fold_c;
     p.rhl = ea.rhl; p.hl_plane = ea.hl_plane;
     p.onetile = ea.onetile ? 1 : 0;
+    p.m_dev = ea.m_dev;
     const double flops = 2.0 * M * N * K;
     // algorithmic bytes: A, W, the residual read (f32 or two bf16 planes: 4 B either way), the output
     // (f32, bf16, or two bf16 planes) and the bf16 copy of EPI_LN_STATS
@@ -536,7 +541,7 @@ bool fold_block(const ce_handle* h, const std::string& p, FoldBlk& f) {
 // w.stats = (mu, rstd) of every row of w.x; the residual GEMMs re-establish both for the next block
 // (the last block of the tower writes f32 w.x instead).
 int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, const FoldBlk& f, int B, int L,
-                     int D, int H, int F, bool last, bool vis = true) {
+                     int D, int H, int F, bool last, bool vis = true, const int* seg = nullptr) {
     const int M = B * L;
     struct PartScope {
         ce_handle* h;
@@ -569,9 +574,12 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     // the text tower's small grids run beside the image tower's persistent GEMMs (second stream):
     // four-wave kernel, one tile per workgroup, so they take CUs a tile at a time
     fold.onetile = st.onetile = last_ea.onetile = !vis;
+    // packed text rows (pooled-only calls): seg[B] live rows of the B * L, sequences by seg
+    const int* m_dev = seg ? seg + B : nullptr;
+    fold.m_dev = st.m_dev = m_dev;
     auto finalize = [&] {
         return timed(h, s, vis ? "ln_stats_v" : "ln_stats_t", 0.0, (double)M * (D / 64) * 8 + (double)M * 8,
-                     [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s); });
+                     [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, M, D / 64, s, m_dev); });
     };
     fold.fold_c = f.cqkv;
     CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
@@ -580,7 +588,7 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         const double flops = 4.0 * B * H * (double)L * L * 64;
         const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
         CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
-                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, !vis, true, s); }));
+                     [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, !vis, true, s, nullptr, seg); }));
     }
     CE_TRY(gemm(h, s, vis ? "gemm_out_v" : "gemm_out_t", w.att, D, k.wout, M, D, D, k.bout, ce::ACT_NONE_, resid,
                 w.x, false, 0, 0, 0, 0, 0, st));
@@ -609,7 +617,7 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
 // compact in w.x [B][D].  Compact work buffers: attention rows, then the residual hi/lo planes, in
 // w.att; LN statistics of the B rows in w.stats / w.stats_part; c_fc output in w.hid.
 int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k, const FoldBlk& f, int B, int L,
-                     int D, int H, int F, const int* sel, bool vis) {
+                     int D, int H, int F, const int* sel, bool vis, const int* seg = nullptr) {
     const int M = B * L;
     struct PartScope {
         ce_handle* h;
@@ -620,6 +628,7 @@ int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     fold.epi = ce::EPI_LN_FOLD;
     fold.fold_stats = w.stats;
     fold.onetile = !vis;
+    fold.m_dev = seg ? seg + B : nullptr;
     fold.fold_c = f.cqkv;
     CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
                 nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
@@ -630,7 +639,7 @@ int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         const double flops = 4.0 * B * H * (double)L * 64;
         const double bytes = (double)M * 2 * D * 2 + (double)B * D * 2 * 4;
         CE_TRY(timed(h, s, vis ? "attn_pool_v" : "attn_pool_t", flops, bytes, [&] {
-            return ce::launch_attention_rows(w.qkv, sel, att, B, L, H, !vis, w.xn, (long)M * D, xc, cplane, s);
+            return ce::launch_attention_rows(w.qkv, sel, att, B, L, H, !vis, w.xn, (long)M * D, xc, cplane, s, seg);
         }));
     }
     EpiArgs st;
@@ -644,6 +653,7 @@ int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     CE_TRY(timed(h, s, vis ? "ln_stats_pool_v" : "ln_stats_pool_t", 0.0, (double)B * (D / 64) * 8 + (double)B * 8,
                  [&] { return ce::launch_ln_stats_finalize(w.stats, w.stats_part, B, D / 64, s); }));
     fold.fold_c = f.cfc;
+    fold.m_dev = nullptr;
     CE_TRY(gemm(h, s, vis ? "gemm_fc_pool_v" : "gemm_fc_pool_t", xc, D, f.wfc, B, F, D, f.dfc, act_code(h), nullptr, w.hid,
                 true, 0, 0, 0, 0, 0, fold));
     EpiArgs last_ea;
@@ -721,27 +731,30 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
     bool use_fold = h->ln_fold && D % 64 == 0 && D / 64 <= 64 && c.text.layers > 0;
     for (int i = 0; use_fold && i < c.text.layers; ++i)
         use_fold = fold_block(h, "transformer.resblocks." + std::to_string(i) + ".", folds[i]);
+    // pooled rows only (no tokens wanted): the last block for the EOT rows alone, and every block on
+    // the packed rows 0..EOT of each caption
+    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && L >= 3;
+    const int* seg = prune ? w.seg : nullptr;
+    if (prune) CE_TRY(check_launch(ce::launch_text_pack(w.rows, w.seg, ids, B, L, s), "text_pack"));
+    else if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     if (use_fold) {
         CE_TRY(timed(h, s, "t_embed", 0.0, (double)B * L * D * (h->resid_hl ? 12.0 : 10.0), [&] {
             return ce::launch_text_embed_stats(w.x, w.xn, h->resid_hl ? w.xlo : nullptr, w.stats, ids,
                                                W(h, "token_embedding.weight"), W(h, "positional_embedding"), B, L, D,
-                                               c.vocab_size, s);
+                                               c.vocab_size, s, seg);
         }));
     } else {
         CE_TRY(check_launch(ce::launch_text_embed(w.x, ids, W(h, "token_embedding.weight"),
                                                   W(h, "positional_embedding"), B, L, D, c.vocab_size, s),
                             "token_embedding"));
     }
-    // pooled rows only (no tokens wanted): the last block for the EOT rows alone
-    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && L >= 3;
-    if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     for (int i = 0; i < c.text.layers; ++i) {
         const Blk k = block_ptrs(h, "transformer.resblocks." + std::to_string(i) + ".");
         const bool last = i + 1 == c.text.layers;
         if (prune && last)
-            CE_TRY(run_block_pooled(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, w.rows, false));
+            CE_TRY(run_block_pooled(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, w.rows, false, seg));
         else if (use_fold)
-            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, last, false));
+            CE_TRY(run_block_folded(h, s, w, k, folds[i], B, L, D, c.text.heads, c.text.mlp_width, last, false, seg));
         else
             CE_TRY(run_block(h, s, w, k, B, L, D, c.text.heads, c.text.mlp_width, true, false));
     }

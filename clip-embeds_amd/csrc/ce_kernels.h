@@ -53,6 +53,9 @@ struct GemmParams {
     // run beside another stream's persistent GEMMs (the text tower beside the image tower) take
     // CUs one tile at a time as they free up (GEMM_VAR_SMALL_ONETILE, default on)
     int onetile = 0;
+    // packed rows (the text tower's pooled-only calls): only the first *m_dev of the M rows are live;
+    // tiles past them exit.  Implies one tile per workgroup and no split-K tail (launch_gemm).
+    const int* m_dev = nullptr;
 };
 // EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)
@@ -60,7 +63,9 @@ enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2, EPI_LN_STATS_HL
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
 // (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
 // combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
-hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s);
+// (m_dev: packed rows, only the first *m_dev of the `rows` are live)
+hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s,
+                                    const int* m_dev = nullptr);
 int set_gemm_schedule(int v);   // returns previous
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
 int set_gemm_variant(int bits);  // kernel-variant bits for A/B (GEMM_VAR_*); returns previous
@@ -82,13 +87,15 @@ constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(
 int set_attn_variant(int var);  // attention forward variant (0-2) for A/B; returns previous
 int set_fgemm_variant(int v);   // 1 = register-blocked f32 GEMM (default), 0 = the 64 x 64 kernel
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s, float* lse = nullptr);   // lse: [B][H][L] log2 log-sum-exp (training)
+                            hipStream_t s, float* lse = nullptr,   // lse: [B][H][L] log2 log-sum-exp (training)
+                            const int* seg = nullptr);  // seg: packed sequences (launch_text_pack), L = max length
 // The same attention for ONE query row per sequence (row qrows[b], absolute; null: row b*L), keys
 // of sequence b only (0..qrows[b]-b*L with causal); out [B][D] bf16 compact.  q pre-scaled as
 // launch_attention(q_prescaled).  src/dst (optional): copy the selected rows of the hi/lo planes
 // (plane strides splane / dplane elements) to compact rows b of dst.
 hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
-                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s);
+                                 const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s,
+                                 const int* seg = nullptr);   // seg: packed causal sequences (row0 = seg[b])
 
 // LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.
 //   in row  = (r / grp) * i_gs + i_go + r % grp   (grp == 0: identity)
@@ -125,7 +132,10 @@ hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, con
 // null: xb = bf16(x)), row (mu, rstd).  D in {256, 512, 768, 1024, 1280}.
 hipError_t launch_text_embed_stats(float* x, bf16_t* xb, bf16_t* xlo, float2* stats, const int64_t* ids,
                                    const float* tok, const float* pos, int B, int ctx, int D, int vocab,
-                                   hipStream_t s);
+                                   hipStream_t s, const int* seg = nullptr);   // seg: packed rows (launch_text_pack)
+// packed text rows of a pooled-only call: caption b's tokens 0..EOT at rows seg[b]..seg[b+1]-1,
+// seg[B] = live rows, sel[b] = seg[b] + EOT position (one workgroup)
+hipError_t launch_text_pack(int* sel, int* seg, const int64_t* ids, int B, int ctx, hipStream_t s);
 // rows[b] = b*ctx + argmax_t ids[b,t]  (first maximal id; EOT is the largest id)
 hipError_t launch_argmax_rows(int* rows, const int64_t* ids, int B, int ctx, hipStream_t s);
 // LayerNorm of gathered rows: out[i] = LN(x + rows[i]*row_stride) (f32); rows == nullptr -> rows[i] = i

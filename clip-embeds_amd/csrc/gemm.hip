@@ -957,6 +957,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     int tm, tn;
     tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
+    // packed rows: clip at the live count, a tile wholly past it exits (no split-K with m_dev)
+    if (p.m_dev) {
+        p.M = min(p.M, __builtin_amdgcn_readfirstlane(*p.m_dev));
+        if (m0 >= p.M) return;
+    }
 
     const int fr = lane & 15;
     const int fq = lane >> 4;
@@ -1524,7 +1529,15 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     // whole rounds only when the host planned a split-K tail (its p.tail tiles run as K-chunks on
     // the 4-phase kernel in tail-only mode, then gemm_splitk_fixup)
     const int t_main = nwg - p.tail;
-    const int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
+    int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
+    // packed rows (one tile per workgroup, forced by the host): clip at the live count; a tile
+    // wholly past it does nothing
+    if (p.m_dev) {
+        p.M = min(p.M, __builtin_amdgcn_readfirstlane(*p.m_dev));
+        int tm, tn;
+        tile_of(min(slot, nwg - 1), tiles_m, tiles_n, p.gm, tm, tn);
+        if (tm * BM >= p.M) my_tiles = 0;
+    }
     const int nsteps = my_tiles * nk;
     const bool nowait = (p.variant & GEMM_VAR_W4PP_NOWAIT) != 0;
     // De-synchronised start (p.stagger, units of s_sleep 16 ~ 1k cycles): equal tiles keep every
@@ -1817,7 +1830,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     // tiles t_main..nwg-1 (a last round of <= grid/8 tiles) run as split-K chunks on the 4-phase
     // kernel + gemm_splitk_fixup (plan_tail_rhl)
     const int t_main = nwg - p.tail;
-    const int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
+    int my_tiles = slot < t_main ? (t_main - 1 - slot) / grid + 1 : 0;
+    // packed rows (one tile per workgroup, forced by the host): clip at the live count
+    if (p.m_dev) {
+        p.M = min(p.M, __builtin_amdgcn_readfirstlane(*p.m_dev));
+        int tm, tn;
+        tile_of(min(slot, nwg - 1), tiles_m, tiles_n, p.gm, tm, tn);
+        if (tm * BM >= p.M) my_tiles = 0;
+    }
     // de-synchronised start (p.stagger x s_sleep 127 for the odd slots): equal tiles keep the CUs in
     // lock-step, K-loops (MFMA-bound) and epilogues (HBM-bound) each chip-wide at once
     if (p.stagger > 0 && (slot & 1))
@@ -2799,6 +2819,13 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     p.variant = gemm_variant();
     p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
+    if (p.m_dev) {
+        // packed rows: the folded-tower epilogues on one tile per workgroup, no split-K
+        if ((epi != EPI_LN_FOLD && epi != EPI_LN_STATS_HL) || gemm_sched() == 12) return hipErrorInvalidValue;
+        p.onetile = 1;
+        p.part = nullptr;
+        p.part_elems = 0;
+    }
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
     if (p.rhl && epi != EPI_LN_STATS_HL && epi != EPI_HL_F32) return hipErrorInvalidValue;

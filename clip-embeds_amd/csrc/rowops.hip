@@ -241,15 +241,22 @@ __global__ __launch_bounds__(256) void text_embed_stats_k(float* __restrict__ x,
                                                           const int64_t* __restrict__ ids,
                                                           const float* __restrict__ tok,
                                                           const float* __restrict__ pos, int rows, int ctx,
-                                                          int vocab) {
+                                                          int vocab, const int* __restrict__ seg) {
     constexpr int D = NC * 256;
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    int64_t id = ids[row];
+    const int prow = blockIdx.x * 4 + (threadIdx.x >> 6);     // padded row b * ctx + t
+    if (prow >= rows) return;
+    const int t = prow % ctx;
+    int row = prow;
+    if (seg) {                                                 // packed: caption b's rows from seg[b]
+        const int b = prow / ctx;
+        if (t >= seg[b + 1] - seg[b]) return;
+        row = seg[b] + t;
+    }
+    int64_t id = ids[prow];
     id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
     const float* tr = tok + (size_t)id * D;
-    const float* pr = pos + (size_t)(row % ctx) * D;
+    const float* pr = pos + (size_t)t * D;
     float4 v[NC];
     float sm = 0.f;
 #pragma unroll
@@ -278,6 +285,50 @@ __global__ __launch_bounds__(256) void text_embed_stats_k(float* __restrict__ x,
         *reinterpret_cast<uint2*>(xb + o) = hi;
         if (xlo) *reinterpret_cast<uint2*>(xlo + o) = lo;
     }
+}
+
+// Packed text rows for pooled-only calls: caption b keeps its rows up to the EOT
+// token (the argmax id, ties to the first, as argmax_rows_k) — under the causal mask no later row
+// reaches the EOT row — at packed rows seg[b] .. seg[b + 1] - 1; seg[B] = the live row count and
+// sel[b] = the packed EOT row.  One workgroup, chunks of 256 captions, block-wide exclusive scan.
+__global__ __launch_bounds__(256) void text_pack_k(int* __restrict__ sel, int* __restrict__ seg,
+                                                   const int64_t* __restrict__ ids, int B, int ctx) {
+    __shared__ int wsum[4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int carry = 0;
+    for (int b0 = 0; b0 < B; b0 += 256) {
+        const int b = b0 + t;
+        int len = 0;
+        if (b < B) {
+            const int64_t* r = ids + (size_t)b * ctx;
+            int64_t best = r[0];
+            int bi = 0;
+            for (int k = 1; k < ctx; ++k) {
+                const int64_t v = r[k];
+                if (v > best) { best = v; bi = k; }
+            }
+            len = bi + 1;
+        }
+        int inc = len;                                   // inclusive scan inside the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int before = carry;
+        for (int w = 0; w < wave; ++w) before += wsum[w];
+        const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (b < B) {
+            const int off = before + inc - len;
+            seg[b] = off;
+            sel[b] = off + len - 1;
+        }
+        carry += total;
+        __syncthreads();
+    }
+    if (t == 0) seg[B] = carry;
 }
 
 __global__ __launch_bounds__(64) void argmax_rows_k(int* rows, const int64_t* ids, int B, int ctx) {
@@ -397,8 +448,9 @@ __global__ __launch_bounds__(256) void f32_to_bf16_k(bf16_t* out, const float* i
 // 16 lanes per row, lane k reading slab k (k, k+16, ...): the row's partials are one coalesced
 // 128-B read for D = 1024; Chan's combine of equal-size (64-column) slabs
 __global__ __launch_bounds__(256) void ln_stats_finalize_k(float2* __restrict__ stats, const float2* __restrict__ part,
-                                                           int rows, int nslab) {
+                                                           int rows, int nslab, const int* __restrict__ m_dev) {
     const int r = blockIdx.x * 16 + (threadIdx.x >> 4), k0 = threadIdx.x & 15;
+    if (m_dev) rows = min(rows, *m_dev);                 // packed rows: the live count
     const bool live = r < rows;
     const float2* pr = part + (size_t)(live ? r : 0) * nslab;
     float2 v[4];
@@ -427,11 +479,12 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_k(float2* __restrict__ 
 
 }  // namespace
 
-hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s) {
+hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s,
+                                    const int* m_dev) {
     if (rows <= 0) return hipSuccess;
     if (nslab <= 0 || nslab > 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ln_stats_finalize_k, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, stats, part, rows,
-                       nslab);
+                       nslab, m_dev);
     return hipGetLastError();
 }
 
@@ -480,16 +533,22 @@ hipError_t launch_text_embed(float* x, const int64_t* ids, const float* tok, con
 
 hipError_t launch_text_embed_stats(float* x, bf16_t* xb, bf16_t* xlo, float2* stats, const int64_t* ids,
                                    const float* tok, const float* pos, int B, int ctx, int D, int vocab,
-                                   hipStream_t s) {
+                                   hipStream_t s, const int* seg) {
     const int rows = B * ctx;
     const dim3 grid((unsigned)((rows + 3) / 4));
     if (!x || !xb || !stats) return hipErrorInvalidValue;
-    if (D == 768) hipLaunchKernelGGL(text_embed_stats_k<3>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
-    else if (D == 512) hipLaunchKernelGGL(text_embed_stats_k<2>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
-    else if (D == 1024) hipLaunchKernelGGL(text_embed_stats_k<4>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
-    else if (D == 1280) hipLaunchKernelGGL(text_embed_stats_k<5>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
-    else if (D == 256) hipLaunchKernelGGL(text_embed_stats_k<1>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab);
+    if (D == 768) hipLaunchKernelGGL(text_embed_stats_k<3>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab, seg);
+    else if (D == 512) hipLaunchKernelGGL(text_embed_stats_k<2>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab, seg);
+    else if (D == 1024) hipLaunchKernelGGL(text_embed_stats_k<4>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab, seg);
+    else if (D == 1280) hipLaunchKernelGGL(text_embed_stats_k<5>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab, seg);
+    else if (D == 256) hipLaunchKernelGGL(text_embed_stats_k<1>, grid, dim3(256), 0, s, x, xb, xlo, stats, ids, tok, pos, rows, ctx, vocab, seg);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_text_pack(int* sel, int* seg, const int64_t* ids, int B, int ctx, hipStream_t s) {
+    if (B <= 0 || ctx <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(text_pack_k, dim3(1), dim3(256), 0, s, sel, seg, ids, B, ctx);
     return hipGetLastError();
 }
 
