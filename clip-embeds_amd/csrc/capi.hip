@@ -469,7 +469,9 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
                          ((resid || hl) ? (double)M * N * 4 : 0.0) +
                          (ea.xb && ea.epi == ce::EPI_LN_STATS ? (double)M * N * 2 : 0.0);
-    return timed(h, s, tag, flops, bytes, [&] { return ce::launch_gemm(p, act, out_bf16, s, ea.epi); });
+    // (packed rows: the live count is known on the device only; the work is not reported)
+    return timed(h, s, tag, ea.m_dev ? 0.0 : flops, ea.m_dev ? 0.0 : bytes,
+                 [&] { return ce::launch_gemm(p, act, out_bf16, s, ea.epi); });
 }
 
 int layernorm(ce_handle* h, hipStream_t s, const char* tag, const float* in, void* out, bool out_bf16,
@@ -585,8 +587,8 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
                 nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
     {
-        const double flops = 4.0 * B * H * (double)L * L * 64;
-        const double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
+        const double flops = seg ? 0.0 : 4.0 * B * H * (double)L * L * 64;
+        const double bytes = seg ? 0.0 : (double)M * 3 * D * 2 + (double)M * D * 2;
         CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
                      [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, !vis, true, s, nullptr, seg); }));
     }

@@ -946,7 +946,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     int wgid, kt0 = 0, kt1 = nk, slab = -1;
     if (SCHED == 1 && p.tail_only) bid += t_main;      // only the split-K chunks (SCHED 11's tail)
     if (bid < t_main) {
-        wgid = xcd_remap(bid, t_main);
+        // (packed rows: the live tiles are the first tile indices; blockIdx order spreads them over
+        // the XCDs round-robin instead of the first XCDs' contiguous ranges)
+        wgid = p.m_dev ? bid : xcd_remap(bid, t_main);
     } else {
         slab = bid - t_main;
         const int c = slab % p.split;
@@ -1524,7 +1526,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     const int tiles_n = (p.N + BN - 1) / BN;
     const int nwg = tiles_m * tiles_n;
     const int grid = gridDim.x;
-    const int slot = xcd_remap(blockIdx.x, grid);
+    // (packed rows: blockIdx order, so the live tiles, the first indices, spread over all XCDs)
+    const int slot = p.m_dev ? (int)blockIdx.x : xcd_remap(blockIdx.x, grid);
     const int nk = p.K / BK;
     // whole rounds only when the host planned a split-K tail (its p.tail tiles run as K-chunks on
     // the 4-phase kernel in tail-only mode, then gemm_splitk_fixup)
@@ -1536,7 +1539,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         p.M = min(p.M, __builtin_amdgcn_readfirstlane(*p.m_dev));
         int tm, tn;
         tile_of(min(slot, nwg - 1), tiles_m, tiles_n, p.gm, tm, tn);
-        if (tm * BM >= p.M) my_tiles = 0;
+        if (tm * BM >= p.M) return;
     }
     const int nsteps = my_tiles * nk;
     const bool nowait = (p.variant & GEMM_VAR_W4PP_NOWAIT) != 0;
@@ -1825,7 +1828,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     const int tiles_n = p.N / BN;
     const int nwg = tiles_m * tiles_n;
     const int grid = gridDim.x;
-    const int slot = xcd_remap(blockIdx.x, grid);
+    // (packed rows: blockIdx order, so the live tiles, the first indices, spread over all XCDs)
+    const int slot = p.m_dev ? (int)blockIdx.x : xcd_remap(blockIdx.x, grid);
     const int nk = p.K / BK;
     // tiles t_main..nwg-1 (a last round of <= grid/8 tiles) run as split-K chunks on the 4-phase
     // kernel + gemm_splitk_fixup (plan_tail_rhl)
@@ -2446,8 +2450,9 @@ void plan_tail(GemmParams& p, int nwg) {
     const int C = num_cus(), nk = p.K / BK;
     if (!splitk_enabled() || !p.part) return;
     int R, cap;
-    if (nwg <= C / 2 && nk >= 32) {
-        // small grid, long K (weight gradients: M = out features, K = tokens): split every tile
+    if ((nwg <= C / 2 && nk >= 32) || (nwg <= C / 16 && nk >= 8)) {
+        // small grid, long K (weight gradients: M = out features, K = tokens), or a grid of a few
+        // tiles (the pooled rows' GEMMs, M = batch): split every tile
         R = nwg;
         cap = 64;
     } else {

@@ -217,7 +217,7 @@ def test_batch256_full_depth_bench_path(full_model, golden):
 def test_batch256_pooled_prune(full_model, golden):
     """The bench's own calls (pooled features only): each tower's last block runs for the pooled
     rows alone (CLS / EOT; ce_set_pooled_prune).  Asserts the paths (23 c_fc on SCHED 11, the
-    pruned B-row c_fc / out-proj on SCHED 1) and checks the pooled outputs against the unpruned
+    pruned B-row c_fc / out-proj on SCHED 1 with split-K over every tile) and checks the pooled outputs against the unpruned
     path (2e-5 cosine: the pruned attention keeps P in f32, the small GEMMs sum in another order)
     and the golden rows against the reference (1e-3)."""
     m = full_model
@@ -227,8 +227,9 @@ def test_batch256_pooled_prune(full_model, golden):
     pi = m.encode_image(imgs)
     torch.cuda.synchronize()
     cnt = path_counts()
-    assert cnt[W4PP + FOLD] == 47 and cnt[NT + FOLD] == 1, cnt
-    assert cnt[W4PP + STATS] == 46 and cnt[NT + STATS] == 1 and cnt[FIXUP + STATS] == 46, cnt
+    # (the pruned B-row GEMMs: 4 / 16 tiles, split-K over every tile + fixup)
+    assert cnt[W4PP + FOLD] == 47 and cnt[NT + FOLD] == 1 and cnt[FIXUP + FOLD] == 1, cnt
+    assert cnt[W4PP + STATS] == 46 and cnt[NT + STATS] == 1 and cnt[FIXUP + STATS] == 47, cnt
     pt = m.encode_text(caps)
     prev = m.engine.set_pooled_prune(False)
     try:
