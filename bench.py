@@ -202,7 +202,10 @@ def build_clip(args, dev, rank, world):
                         "(BASELINE configs[1]: batch 256/GPU bf16)",
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}",
-            "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none"}
+            "exchange": "RCCL all_gather of L2-normalised embeddings" if world > 1 else "none",
+            "rows": ("every row" if args.no_pooled_prune else
+                     "pooled-only calls: image last block for the CLS rows, text on rows 0..EOT (packed), "
+                     "its last block for the EOT rows; outputs = the full computation's")}
     pi, pt = pooled_prune_flops(cfg, not args.no_pooled_prune, caps.cpu().numpy().argmax(1))
     return dict(engine=model.engine, step=step, pairs=B, flops_per_pair=FLOPS_PER_PAIR, sd=sd, cfg=cfg,
                 flops_exec_per_pair=FLOPS_PER_PAIR - pi - pt,
