@@ -511,16 +511,21 @@ int g_attn_var = 125;
 // One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
 // mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
 // of the image tower, the EOT row qrows[b] of the text tower).  Workgroup =
-// (head, batch), 256 threads: scores with one key per thread (the row's 128 B as eight 16-B
-// loads), block max / sum, then P.V with 16 key slots x 16 four-column groups and a fixed-order
-// slot sum.  Same arithmetic as attn_fwd where it matters: q arrives pre-scaled by log2(e)/8 (the
-// engine's in_proj weights), scores in log2 units, p = exp2(s - max); P stays f32 here.
-// Optionally copies the selected row's 64 columns of the hi/lo residual planes to compact planes
-// (the residual of the pruned out-projection).
+// (head, batch), 256 threads: scores with four lanes per key (32 B each, two lane-pair sums),
+// block max / sum, then P.V with 16 key slots x 16 four-column groups and a fixed-order slot sum.
+// Same arithmetic as attn_fwd where it matters: q pre-scaled by log2(e)/8 (the engine's in_proj
+// weights), scores in log2 units, p = exp2(s - max); P stays f32 here.
+// wq (optional): the pooled row's q is computed here instead of read from qkv (the QKV GEMM then
+// covers only K and V): the LN-folded in_proj of that row, q = rstd (x W'^T - mu c) + d rounded to
+// bf16 as the GEMM's output, with x = the hi plane row (src), (mu, rstd) = stats[row].
+// src/dst (optional): copies the pooled row's 64 columns of the hi/lo residual planes to compact
+// planes (the residual of the pruned out-projection).
 __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qkv, const int* __restrict__ qrows,
                                                    int L, int H, int causal, bf16_t* __restrict__ out,
                                                    const bf16_t* __restrict__ src, long splane,
-                                                   bf16_t* __restrict__ dst, long dplane, const int* __restrict__ seg) {
+                                                   bf16_t* __restrict__ dst, long dplane, const int* __restrict__ seg,
+                                                   const bf16_t* __restrict__ wq, const float* __restrict__ cq,
+                                                   const float* __restrict__ dq, const float2* __restrict__ stats) {
     extern __shared__ float sc[];                 // [L]: scores, then probabilities
     __shared__ float qs[64];
     __shared__ float red[2][4];
@@ -532,27 +537,64 @@ __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qk
     const long qr = qrows ? (long)qrows[b] : row0;
     const int nk = causal ? (int)(qr - row0) + 1 : L;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    if (t < 64) qs[t] = bf2f(qkv[qr * ld + h * 64 + t]);
+    if (wq) {
+        // q[j]: wave w takes columns j = 16w .. 16w + 15, each a dot product of the whole row over
+        // the wave (lane l: 16-B chunks l, l + 64, ... of x and of W' row j: coalesced 1-KB loads)
+        const int nch = D / 8;
+        const uint4* xr = reinterpret_cast<const uint4*>(src + qr * D);
+        uint4 xv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xv[c] = (lane + 64 * c < nch) ? xr[lane + 64 * c] : make_uint4(0u, 0u, 0u, 0u);
+        for (int jj = 0; jj < 16; ++jj) {
+            const int j = wave * 16 + jj;
+            const uint4* wr = reinterpret_cast<const uint4*>(wq + (long)(h * 64 + j) * D);
+            float a = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (lane + 64 * c < nch) {
+                    const uint4 w = wr[lane + 64 * c], x = xv[c];
+                    const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        a = fmaf(__uint_as_float(xs[e] << 16), __uint_as_float(ws[e] << 16), a);
+                        a = fmaf(__uint_as_float(xs[e] & 0xffff0000u), __uint_as_float(ws[e] & 0xffff0000u), a);
+                    }
+                }
+            }
+            a = wave_sum(a);
+            if (lane == 0) {
+                const float2 st = stats[qr];
+                const int n = h * 64 + j;
+                qs[j] = bf2f(f2bf(fmaf(st.y, fmaf(-st.x, cq[n], a), dq[n])));
+            }
+        }
+    } else if (t < 64) {
+        qs[t] = bf2f(qkv[qr * ld + h * 64 + t]);
+    }
     if (src && t < 128) {
         const int pl = t >> 6;
         dst[pl * dplane + (long)b * D + h * 64 + lane] = src[pl * splane + qr * D + h * 64 + lane];
     }
     __syncthreads();
+    // scores: key j = t / 4 + 64 i, dims (t & 3) * 16 .. + 15 of it per lane
     float m = -INFINITY;
-    for (int j = t; j < nk; j += 256) {
-        const uint4* kp = reinterpret_cast<const uint4*>(qkv + (row0 + j) * ld + D + h * 64);
+    const int part = t & 3;
+    float qp[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) qp[e] = qs[part * 16 + e];
+    for (int j = t >> 2; j < nk; j += 64) {
+        const uint4* kp = reinterpret_cast<const uint4*>(qkv + (row0 + j) * ld + D + h * 64 + part * 16);
+        const uint4 u0 = kp[0], u1 = kp[1];
+        const uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
         float s = 0.f;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint4 u = kp[c];
-            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                s = fmaf(qs[c * 8 + 2 * e], __uint_as_float(w[e] << 16), s);
-                s = fmaf(qs[c * 8 + 2 * e + 1], __uint_as_float(w[e] & 0xffff0000u), s);
-            }
+        for (int e = 0; e < 8; ++e) {
+            s = fmaf(qp[2 * e], __uint_as_float(w[e] << 16), s);
+            s = fmaf(qp[2 * e + 1], __uint_as_float(w[e] & 0xffff0000u), s);
         }
-        sc[j] = s;
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if (part == 0) sc[j] = s;
         m = fmaxf(m, s);
     }
     m = wave_max(m);
@@ -594,12 +636,14 @@ __global__ __launch_bounds__(256) void attn_rows_k(const bf16_t* __restrict__ qk
 
 hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
                                  const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s,
-                                 const int* seg) {
+                                 const int* seg, const bf16_t* wq, const float* cq, const float* dq,
+                                 const float2* stats) {
     if (B <= 0 || L <= 0) return hipSuccess;
     if ((size_t)L * 4 > 96 * 1024 || B > 65535) return hipErrorInvalidValue;
     if (seg && (!qrows || !causal)) return hipErrorInvalidValue;
+    if (wq && (!src || !cq || !dq || !stats || H * 64 > 4 * 64 * 8)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(attn_rows_k, dim3(H, B), dim3(256), (size_t)L * 4, s, qkv, qrows, L, H, causal ? 1 : 0, out,
-                       src, splane, dst, dplane, seg);
+                       src, splane, dst, dplane, seg, wq, cq, dq, stats);
     return hipGetLastError();
 }
 

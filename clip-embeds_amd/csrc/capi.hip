@@ -444,6 +444,7 @@ struct EpiArgs {
     long hl_plane = 0;
     bool onetile = false;            // one tile per four-wave workgroup (the text tower's small grids)
     const int* m_dev = nullptr;      // packed rows: live row count on the device
+    long ldo = 0;                    // output row stride (0: N)
 };
 
 int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* Wt,
@@ -454,7 +455,7 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     p.M = M; p.N = N; p.K = K;
     p.bias = bias;
     p.resid = resid; p.ldr = N;
-    p.out = out; p.ldo = N;
+    p.out = out; p.ldo = ea.ldo ? ea.ldo : N;
     p.grp = grp; p.o_gs = o_gs; p.o_go = o_go; p.r_gs = r_gs; p.r_go = r_go;
     p.part = h->cur_part;            // split-K tail slabs of the tower being run (null: no split)
     p.part_elems = h->cur_part ? ce::kGemmPartElems : 0;
@@ -631,9 +632,20 @@ int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     fold.fold_stats = w.stats;
     fold.onetile = !vis;
     fold.m_dev = seg ? seg + B : nullptr;
-    fold.fold_c = f.cqkv;
-    CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
-                nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
+    // image tower: K and V of every row (in_proj rows D..3D into qkv's K | V thirds), the pooled
+    // rows' q computed inside the attention kernel (the q third of 147,712 rows is 0.28 ms); text
+    // tower (a few thousand packed rows): the whole QKV GEMM, cheaper than 64 W' rows per workgroup
+    if (vis) {
+        fold.fold_c = f.cqkv + D;
+        fold.ldo = 3L * D;
+        CE_TRY(gemm(h, s, "gemm_kv_pool_v", w.xn, D, f.wqkv + (size_t)D * D, M, 2 * D, D, f.dqkv + D, ce::ACT_NONE_,
+                    nullptr, w.qkv + D, true, 0, 0, 0, 0, 0, fold));
+        fold.ldo = 0;
+    } else {
+        fold.fold_c = f.cqkv;
+        CE_TRY(gemm(h, s, "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_, nullptr, w.qkv, true,
+                    0, 0, 0, 0, 0, fold));
+    }
     bf16_t* att = w.att;                          // [B][D]
     bf16_t* xc = w.att + (size_t)B * D;           // hi plane [B][D], lo plane after it
     const long cplane = (long)B * D;
@@ -641,7 +653,8 @@ int run_block_pooled(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
         const double flops = 4.0 * B * H * (double)L * 64;
         const double bytes = (double)M * 2 * D * 2 + (double)B * D * 2 * 4;
         CE_TRY(timed(h, s, vis ? "attn_pool_v" : "attn_pool_t", flops, bytes, [&] {
-            return ce::launch_attention_rows(w.qkv, sel, att, B, L, H, !vis, w.xn, (long)M * D, xc, cplane, s, seg);
+            return ce::launch_attention_rows(w.qkv, sel, att, B, L, H, !vis, w.xn, (long)M * D, xc, cplane, s, seg,
+                                             vis ? f.wqkv : nullptr, f.cqkv, f.dqkv, w.stats);
         }));
     }
     EpiArgs st;

@@ -95,7 +95,12 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 // (plane strides splane / dplane elements) to compact rows b of dst.
 hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* out, int B, int L, int H, bool causal,
                                  const bf16_t* src, long splane, bf16_t* dst, long dplane, hipStream_t s,
-                                 const int* seg = nullptr);   // seg: packed causal sequences (row0 = seg[b])
+                                 const int* seg = nullptr,    // seg: packed causal sequences (row0 = seg[b])
+                                 // wq: compute the pooled rows' q here (LN-folded in_proj rows 0..D-1 [D][D],
+                                 // fold column sums cq, bias dq, row stats; x = src hi plane); qkv then
+                                 // needs only its K and V thirds
+                                 const bf16_t* wq = nullptr, const float* cq = nullptr, const float* dq = nullptr,
+                                 const float2* stats = nullptr);
 
 // LayerNorm over rows of width D (eps 1e-5, affine), f32 in, f32 or bf16 out.
 //   in row  = (r / grp) * i_gs + i_go + r % grp   (grp == 0: identity)
