@@ -1,0 +1,61 @@
+"""HBM bytes per launch of the bench's kernels from two rocprofv3 --pmc passes over bench.py itself
+(tools/gpu_run.sh steps pmc:FETCH_SIZE and pmc:WRITE_SIZE; MI355X_MICROARCH.md §HBM: separate
+passes, FETCH_SIZE doubled on gfx950, counters in KB).  Dispatches are grouped by kernel name and
+grid size (the image tower's persistent GEMMs run 256 workgroups, the text tower's one-tile GEMMs
+one per tile), so a bench tag maps to one group.
+
+    python tools/pmc_bench_traffic.py gpurun_out/<tag>_pmc1_FETCH_SIZE gpurun_out/<tag>_pmc2_WRITE_SIZE \
+        [profiles/pmc_traffic.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# bench tag -> (kernel-name prefix, grid size in threads) of the image tower at B = 256
+TAGS = {"gemm_fc_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<1, false, true, 2", 65536),
+        "gemm_qkv_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<0, false, true, 2", 65536),
+        "attn_v": ("void ce::(anonymous namespace)::attn_fwd<false", None)}
+
+
+def load(d, counter):
+    g = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] == counter:
+                    g[(row["Kernel_Name"], int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
+    return g
+
+
+def main():
+    fd, wd = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else None
+    fetch, write = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
+    for (k, grid), v in sorted(fetch.items(), key=lambda kv: -sum(kv[1]))[:16]:
+        w = write.get((k, grid), [])
+        print(f"{k[:70]:<70} grid {grid:8d} n {len(v):3d}/{len(w):3d} fetch x2 {2 * sum(v) / len(v) / 1024:9.1f} MB"
+              f"  write {sum(w) / max(1, len(w)) / 1024:8.1f} MB")
+    if not out:
+        return
+    res = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            res = json.load(f)
+    for tag, (pref, grid) in TAGS.items():
+        fs = [v for (k, g), vs in fetch.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
+        ws = [v for (k, g), vs in write.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
+        if not fs or not ws:
+            continue
+        f2, wr = 2 * sum(fs) / len(fs) * 1024, sum(ws) / len(ws) * 1024
+        res[tag] = {"hbm_bytes_per_launch": round(f2 + wr), "fetch_bytes_corrected": round(f2),
+                    "write_bytes": round(wr), "dispatches": [len(fs), len(ws)],
+                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over bench.py, {fd}, {wd}"}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
