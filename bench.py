@@ -314,7 +314,7 @@ def build_sparc(args, dev, rank, world):
             "batch_per_gpu": B, "global_batch": world * B, "tokens": T, "patches": P, "dim": D,
             "parallelism": f"dp{world}", "exchange": "none (per-GPU SparcLoss)"}
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
-                flops_per_pair=IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D,
+                flops_per_pair=IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D, prunable=False,
                 metric="SPARC image-text pairs/sec ViT-L/14-336", config=cfgd)
 
 
@@ -340,6 +340,8 @@ def main():
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM variant bits for A/B (-1 = default)")
     ap.add_argument("--no-pooled-prune", action="store_true",
                     help="run every tower's last block for all rows (A/B of ce_set_pooled_prune)")
+    ap.add_argument("--no-every-row", action="store_true",
+                    help="skip the second timed leg with the pooled prune off (`every_row` in the JSON line)")
     ap.add_argument("--gemm-stagger", type=int, default=-1,
                     help="first-round stagger of the persistent residual GEMMs (x s_sleep 127, odd slots; A/B)")
     args = ap.parse_args()
@@ -409,6 +411,31 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # the same K steps with every row of the last blocks computed (pooled prune off):
+    # reported beside `value` so the step is also measured without the dead-row skipping
+    every_row = None
+    if W.get("prunable", True) and not args.no_pooled_prune and not args.no_every_row:
+        prev = engine.set_pooled_prune(False)
+        step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el2 = time.perf_counter() - t1
+        engine.set_pooled_prune(prev)
+        if world > 1:
+            t = torch.tensor([el2], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        v2 = world * B * args.steps / el2
+        every_row = {"value": round(v2, 2), "ms_per_step": round(1000 * el2 / args.steps, 3),
+                     "model_flops_frac": round(v2 * W["flops_per_pair"] / 1e12 / world / PEAK_BF16_TFLOPS, 4)}
 
     if rank != 0:
         if world > 1:
@@ -481,6 +508,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if every_row:
+        out["every_row"] = every_row
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
