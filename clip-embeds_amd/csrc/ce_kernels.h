@@ -61,6 +61,9 @@ struct GemmParams {
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)
 enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2, EPI_LN_STATS_HL = 3, EPI_HL_F32 = 4 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
+// SCHED 13 (gemm_db.hip): bf16 output without residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0,
+// K >= 1024; `grid` persistent workgroups (p.gm set by the caller)
+hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipStream_t s);
 // (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
 // combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
 // (m_dev: packed rows, only the first *m_dev of the `rows` are live)

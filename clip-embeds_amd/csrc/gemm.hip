@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 #include <atomic>
 #include <cstdlib>
 
@@ -2402,7 +2403,7 @@ int gemm_sched() {
         const char* e = getenv("CE_GEMM_SCHED");
         g_sched = e ? atoi(e) : 1;
         if (!(g_sched == 0 || g_sched == 1 || g_sched == 2 || g_sched == 3 || g_sched == 4 || g_sched == 6 ||
-              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11 || g_sched == 12))
+              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11 || g_sched == 12 || g_sched == 13))
             g_sched = 1;
     }
     return g_sched;
@@ -2580,6 +2581,24 @@ void set_stagger_1(GemmParams& p, int nwg) {
     p.stagger_bit = 3;
 }
 
+// SCHED 13 (gemm_db.hip): bf16 output without residual, whole 128-column tiles, >= 16 K-tiles, full rows
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
+bool db_ok(const GemmParams& p) {
+    if constexpr (!OUT_BF16 || HAS_RESID || !(EPI == EPI_PLAIN || EPI == EPI_LN_FOLD)) return false;
+    else return gemm_sched() == 13 && p.N % 128 == 0 && p.K >= 16 * BK && !p.m_dev && !p.onetile && p.grp == 0;
+}
+
+template <int ACT, int EPI>
+hipError_t launch_db(const GemmParams& p0, hipStream_t s) {
+    GemmParams p = p0;
+    p.gm = gemm_groupm();
+    p.tail = 0;
+    p.split = 1;
+    const int nwg = ((p.M + BM - 1) / BM) * (p.N / 128);
+    count_path(GEMM_PATH_OTHER);
+    return launch_gemm_db(p, ACT, EPI, w4pp_grid(nwg), s);
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_w2(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
@@ -2633,6 +2652,8 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             return hipGetLastError();
         }
     }
+    if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
+        if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p)) return launch_db<ACT, EPI>(p, s);
     if (!HL && gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     if (!HL && (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
         p.gm = gemm_groupm();
@@ -2690,6 +2711,8 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
     p.gm = gemm_groupm();
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    if constexpr (OUT_BF16 && !HAS_RESID)
+        if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p)) return launch_db<ACT, EPI_PLAIN>(p, s);
     const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : gemm_sched();
     if (sc == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
     p.tail = 0;
@@ -2807,7 +2830,7 @@ int set_gemm_schedule(int v) {
     if (ring >= 2 && ring <= 5) g_ring = ring;
     if (st) g_stagger = st - 1;
     g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 || sc == 11 ||
-               sc == 12) ? sc : 1;
+               sc == 12 || sc == 13) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }

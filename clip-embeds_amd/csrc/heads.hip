@@ -189,6 +189,122 @@ __global__ __launch_bounds__(256) void fgemm2_k(FGemmParams p) {
         }
 }
 
+// ---- short-M batched f32 GEMM (SPARC's einsums: M = T = 77 rows per sample) -------------------
+// 80 x 192 output tile per 256-thread block on v_mfma_f32_16x16x4_f32: 16-row granularity, so
+// M = 77 fills 96 % of the rows (32-row blocks: 80 % at 96 rows), and 192 columns divide both
+// N = 576 (P) and N = 768 (D).  Wave w owns columns 48w .. 48w+47 and all 80 rows: 5 x 3
+// accumulators, so per k-step 5 A and 3 B values feed 15 MFMAs.  Within a K chunk of 32 the
+// k index of lane group g = lane >> 4 at k-step s is 8g + s (any k assignment works when A and B
+// share it), so a lane's 8 k-values of a row are contiguous: two ds_read_b128 per row per chunk,
+// and the LDS image is the natural [row][k] layout (rows padded to 36 floats: the 16 rows of a
+// read group start on distinct 4-bank groups).  The next chunk's float4 global loads are in flight
+// under the current chunk's MFMAs.
+constexpr int G3_BM = 80, G3_BN = 192, G3_BK = 32, G3_LD = G3_BK + 4;
+constexpr int G3_NA = (G3_BM * G3_BK / 4 + 255) / 256;        // float4 per thread: A 640 -> 3
+constexpr int G3_NB = G3_BN * G3_BK / 4 / 256;                // B 1536 -> 6
+
+template <bool B_NK>
+__global__ __launch_bounds__(256) void fgemm3_k(FGemmParams p) {
+    __shared__ __attribute__((aligned(16))) float As[G3_BM][G3_LD];
+    __shared__ __attribute__((aligned(16))) float Bs[G3_BN][G3_LD];
+    const int z = blockIdx.z;
+    const float* A = p.A + (size_t)z * p.sA;
+    const float* Bm = p.B + (size_t)z * p.sB;
+    float* C = p.C + (size_t)z * p.sC;
+    const int i0 = blockIdx.y * G3_BM, j0 = blockIdx.x * G3_BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    f32x4 acc[5][3];
+#pragma unroll
+    for (int a = 0; a < 5; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 ra[G3_NA], rb[G3_NB];
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < G3_NA; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, kq = (e & 7) * 4;
+            const int gi = i0 + row, gk = k0 + kq;
+            ra[u] = (row < G3_BM && gi < p.M && gk < p.K) ? *reinterpret_cast<const float4*>(A + (size_t)gi * p.lda + gk) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < G3_NB; ++u) {
+            const int e = tid + 256 * u;
+            if constexpr (B_NK) {
+                const int row = e >> 3, kq = (e & 7) * 4;
+                const int gj = j0 + row, gk = k0 + kq;
+                rb[u] = (gj < p.N && gk < p.K) ? *reinterpret_cast<const float4*>(Bm + (size_t)gj * p.ldb + gk) : z4;
+            } else {
+                const int kk = e / (G3_BN / 4), nq = (e % (G3_BN / 4)) * 4;
+                const int gj = j0 + nq, gk = k0 + kk;
+                rb[u] = (gj < p.N && gk < p.K) ? *reinterpret_cast<const float4*>(Bm + (size_t)gk * p.ldb + gj) : z4;
+            }
+        }
+    };
+    auto store = [&] {
+#pragma unroll
+        for (int u = 0; u < G3_NA; ++u) {
+            const int e = tid + 256 * u, row = e >> 3, kq = (e & 7) * 4;
+            if (row < G3_BM) *reinterpret_cast<float4*>(&As[row][kq]) = ra[u];
+        }
+#pragma unroll
+        for (int u = 0; u < G3_NB; ++u) {
+            const int e = tid + 256 * u;
+            if constexpr (B_NK) {
+                const int row = e >> 3, kq = (e & 7) * 4;
+                *reinterpret_cast<float4*>(&Bs[row][kq]) = rb[u];
+            } else {
+                const int kk = e / (G3_BN / 4), nq = (e % (G3_BN / 4)) * 4;
+                Bs[nq][kk] = rb[u].x; Bs[nq + 1][kk] = rb[u].y; Bs[nq + 2][kk] = rb[u].z; Bs[nq + 3][kk] = rb[u].w;
+            }
+        }
+    };
+    const int g = lane >> 4, m = lane & 15;
+    load(0);
+    for (int k0 = 0; k0 < p.K; k0 += G3_BK) {
+        store();
+        __syncthreads();
+        if (k0 + G3_BK < p.K) load(k0 + G3_BK);
+#pragma unroll
+        for (int hq = 0; hq < 2; ++hq) {             // k-steps 4hq .. 4hq+3: one ds_read_b128 per row
+            float4 a4[5], b4[3];
+#pragma unroll
+            for (int ib = 0; ib < 5; ++ib) a4[ib] = *reinterpret_cast<const float4*>(&As[ib * 16 + m][8 * g + 4 * hq]);
+#pragma unroll
+            for (int jb = 0; jb < 3; ++jb)
+                b4[jb] = *reinterpret_cast<const float4*>(&Bs[wave * 48 + jb * 16 + m][8 * g + 4 * hq]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int ib = 0; ib < 5; ++ib)
+#pragma unroll
+                    for (int jb = 0; jb < 3; ++jb) {
+                        const float av = s == 0 ? a4[ib].x : s == 1 ? a4[ib].y : s == 2 ? a4[ib].z : a4[ib].w;
+                        const float bv = s == 0 ? b4[jb].x : s == 1 ? b4[jb].y : s == 2 ? b4[jb].z : b4[jb].w;
+                        acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ib][jb], 0, 0, 0);
+                    }
+        }
+        __syncthreads();
+    }
+    // D: lane holds column m of its 16-column block, rows 4g .. 4g+3 of each 16-row block
+#pragma unroll
+    for (int jb = 0; jb < 3; ++jb) {
+        const int gj = j0 + wave * 48 + jb * 16 + m;
+        if (gj >= p.N) continue;
+        const float bj = p.bias ? p.bias[gj] : 0.f;
+#pragma unroll
+        for (int ib = 0; ib < 5; ++ib)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i0 + ib * 16 + 4 * g + r;
+                if (gi >= p.M) continue;
+                const float v = acc[ib][jb][r] * p.alpha + bj;
+                C[(size_t)gi * p.ldc + gj] = v;
+                if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
+            }
+    }
+}
+
 // ---- fused PACL pooling -----------------------------------------------------------------
 // Two passes.  Pass 1 (pacl_pool_part_k): grid = R output rows x S patch splits; each 256-thread
 // workgroup streams its P/S patches of one image, one patch row per wave at a time, every lane
@@ -405,13 +521,16 @@ __global__ __launch_bounds__(256) void sparc_weights_k(float* sim, long rows, in
     for (int p = lane; p < P; p += 64) r[p] = r[p] / s;
 }
 
-int g_fgemm2 = 1;     // register-blocked f32 GEMM (0: the 64 x 64 scalar-staged kernel, for A/B)
+// f32 GEMM variant: 0 = the 64 x 64 scalar-staged kernel; 1 (default) = the register-blocked 96 x 128
+// kernel; 2 = as 1, with the short-M 80 x 192 kernel for batched products of M <= 80 rows (measured
+// slower at the C5 shapes: sparc_sim 51.5 vs 62.9 TF/s, sparc_group 59.3 vs 71.1; kept for A/B)
+int g_fgemm2 = 1;
 
 }  // namespace
 
 int set_fgemm_variant(int v) {
     const int prev = g_fgemm2;
-    g_fgemm2 = v != 0;
+    g_fgemm2 = v < 0 ? 0 : v > 2 ? 2 : v;
     return prev;
 }
 
@@ -422,6 +541,12 @@ hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s) {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     const bool vec = p.K % 4 == 0 && p.lda % 4 == 0 && p.ldb % 4 == 0 && p.sA % 4 == 0 && p.sB % 4 == 0 &&
                      al(p.A) && al(p.B) && (b_nk || p.N % 4 == 0);
+    if (vec && g_fgemm2 == 2 && p.M <= G3_BM && p.N >= G3_BN && p.batch > 1) {
+        const dim3 grid((p.N + G3_BN - 1) / G3_BN, 1, p.batch);
+        if (b_nk) hipLaunchKernelGGL(fgemm3_k<true>, grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(fgemm3_k<false>, grid, dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     if (vec && g_fgemm2) {
         const dim3 grid((p.N + G2_BN - 1) / G2_BN, (p.M + G2_BM - 1) / G2_BM, p.batch);
         if (b_nk) hipLaunchKernelGGL(fgemm2_k<true>, grid, dim3(256), 0, s, p);

@@ -290,8 +290,10 @@ int ce_set_gemm_variant(int bits);
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
- * register-blocked 96 x 128 kernel (default, for 16-B aligned operands with K % 4 == 0), 0 = the
- * 64 x 64 scalar-staged kernel.  Returns the previous setting.  For A/B and parity tests. */
+ * register-blocked 96 x 128 kernel (default; 16-B aligned operands with K % 4 == 0); 2 = as 1, and
+ * for batched products of M <= 80 rows and N >= 192 (SPARC's T = 77 rows per sample) the 80 x 192
+ * short-M kernel on v_mfma_f32_16x16x4_f32; 0 = the 64 x 64 scalar-staged kernel.  Returns the
+ * previous setting.  For A/B and parity tests. */
 int ce_set_fgemm_variant(int v);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
  * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other

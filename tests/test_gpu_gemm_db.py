@@ -1,0 +1,113 @@
+"""SCHED 13 (gemm_db, csrc/gemm.hip): the persistent four-wave GEMM with two accumulator sets, whose
+tile t epilogue runs as 16 sub-chunks inside tile t+1's K-loop.  Checked against plain PyTorch f32
+references of the same op (bias / GELU / QuickGELU, LN-folded consumer), with several tiles per
+workgroup, a ragged last M tile, K = 4096 (K-tiles past the 16 that carry sub-chunks) and grids
+smaller than the CU count; rows past M must stay untouched."""
+import ctypes
+
+import pytest
+import torch
+
+from clipembed import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def path_counts():
+    c = (ctypes.c_int64 * 13)()
+    _lib.call("ce_gemm_path_counts", c, 13, 1)
+    return list(c)
+
+
+def run_db(fn):
+    L = _lib.lib()
+    prev = L.ce_set_gemm_schedule(13)
+    try:
+        path_counts()
+        fn()
+        torch.cuda.synchronize()
+        return path_counts()
+    finally:
+        L.ce_set_gemm_schedule(prev)
+
+
+SHAPES = [(20000, 3072, 1024), (2308, 4096, 1024), (17000, 1024, 4096), (300, 1024, 1024), (5, 768, 1024),
+          (65536, 1024, 1024)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_db_bias_act(M, N, K, act):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + act)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    out = torch.full((M + 64, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    cnt = run_db(lambda: _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), act, None, P(out),
+                                   _lib.CE_BF16))
+    assert cnt[9] == 1, cnt                                     # GEMM_PATH_OTHER: the SCHED 13 kernel
+    ref = A.float() @ W.float().t() + bias
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    elif act == 2:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    err = (out[:M].float() - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item() + 1e-5, err
+    assert bool((out[M:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,N", [(20000, 3072), (20000, 4096), (4252, 4096), (300, 1024)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_db_ln_fold(M, N, act):
+    """out = act(rstd_m (A W^T - mu_m c_n) + d_n), the QKV / c_fc epilogue of the folded tower."""
+    K = 1024
+    g = torch.Generator(device="cpu").manual_seed(M + N + act + 13)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    mu = (torch.randn(M, generator=g) * 0.2).to(DEV)
+    rstd = (torch.rand(M, generator=g) * 1.5 + 0.5).to(DEV)
+    stats = torch.stack([mu, rstd], 1).contiguous()
+    fold_c = W.float().sum(1).contiguous()
+    out = torch.full((M + 64, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    cnt = run_db(lambda: _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), act, None, P(out),
+                                   _lib.CE_BF16, 2, None, None, P(stats), P(fold_c)))
+    assert cnt[9] == 1, cnt
+    ref = rstd[:, None] * (A.float() @ W.float().t() - mu[:, None] * fold_c[None, :]) + bias
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    err = (out[:M].float() - ref).abs().max().item()
+    assert err <= 8e-3 * ref.abs().max().item() + 1e-5, err
+    assert bool((out[M:] == 7.0).all())
+
+
+def test_gemm_db_matches_sched11():
+    """Same inputs through SCHED 11 and SCHED 13 (QKV shape at B = 32): both f32-accumulated over
+    the same K order per output, so the bf16 outputs agree to the rounding of the epilogue."""
+    M, N, K = 32 * 577, 3072, 1024
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    outs = []
+    L = _lib.lib()
+    for sc in (11, 13):
+        prev = L.ce_set_gemm_schedule(sc)
+        try:
+            out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            _lib.call("ce_kernel_gemm_bf16", S(), P(A), P(W), M, N, K, P(bias), 1, None, P(out), _lib.CE_BF16)
+            torch.cuda.synchronize()
+            outs.append(out.float())
+        finally:
+            L.ce_set_gemm_schedule(prev)
+    d = (outs[0] - outs[1]).abs().max().item()
+    assert d <= 1e-2 * outs[0].abs().max().item(), d

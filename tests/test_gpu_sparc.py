@@ -88,16 +88,16 @@ def test_sparc_align_precomputed_embeddings_vs_oracle(models):
 
 @pytest.mark.parametrize("B,T,P,D", [(64, 77, 576, 768), (3, 5, 40, 128), (2, 77, 576, 1024)])
 def test_fgemm_variants_agree(models, B, T, P, D):
-    """The register-blocked f32 GEMM (default: SPARC's similarity and grouping einsums, pacl.py:460,
-    472) vs the 64 x 64 kernel it replaced, on the same inputs (both k-ordered chains of
-    v_mfma_f32_32x32x2_f32), and vs the oracle; ragged M / N / K tiles and D = 1024."""
+    """The short-M 80 x 192 f32 GEMM (default for SPARC's similarity and grouping einsums,
+    pacl.py:460,472: v_mfma_f32_16x16x4_f32) and the register-blocked 96 x 128 kernel vs the 64 x 64
+    kernel, on the same inputs, and vs the oracle; ragged M / N / K tiles and D = 1024."""
     from clipembed import _lib
     m = models["sparc"]
     rng = np.random.default_rng(B * 7 + D)
     v = torch.from_numpy((rng.standard_normal((B, P, D)) * 0.5).astype(np.float32)).cuda()
     l = torch.from_numpy((rng.standard_normal((B, T, D)) * 0.5).astype(np.float32)).cuda()
     res = {}
-    for var in (1, 0):
+    for var in (2, 1, 0):
         prev = _lib.lib().ce_set_fgemm_variant(var)
         try:
             gr, ln = m.align(v, l)
@@ -106,7 +106,9 @@ def test_fgemm_variants_agree(models, B, T, P, D):
             _lib.lib().ce_set_fgemm_variant(prev)
         res[var] = (gr.cpu().numpy(), ln.cpu().numpy())
     # (a similarity within an f32 rounding of the threshold may land on the other side: 1e-4)
-    np.testing.assert_allclose(res[1][0], res[0][0], atol=1e-4)
-    np.testing.assert_allclose(res[1][1], res[0][1], atol=1e-7)
+    for var in (2, 1):
+        np.testing.assert_allclose(res[var][0], res[0][0], atol=1e-4)
+        np.testing.assert_allclose(res[var][1], res[0][1], atol=1e-7)
     rg, rl, _ = O.sparc_forward(v.cpu().numpy(), l.cpu().numpy(), 1.0 / 576)
-    np.testing.assert_allclose(res[1][0], rg, atol=1e-4)
+    for var in (2, 1):
+        np.testing.assert_allclose(res[var][0], rg, atol=1e-4)
