@@ -5,14 +5,16 @@
 // staged-residual kernel serialise every epilogue with the matrix pipe idle (c_fc: ~8 of ~32 us per
 // tile; out-proj: ~19 of ~50 us).  Here a workgroup owns 256 x 128 tiles (waves 2 x 2 of
 // 128 x 64: acc[8][4], 128 AGPRs) and keeps TWO accumulator sets: tile t accumulates into set t & 1
-// while the set of tile t-1 is drained in 16 sub-chunks (fragment row c >> 1, column fragments
-// 2 (c & 1) and 2 (c & 1) + 1), one per K-tile 0..15 of tile t, as micro-steps of a few VALU ops
-// placed one per MFMA gap (sched_barrier-pinned) and two 8-B stores per K-tile instead of a burst.
+// while the set of tile t-1 is drained in 16 sub-chunks (fragment rows 2 (c >> 2) and 2 (c >> 2) + 1,
+// column fragment c & 3), one per K-tile 0..15 of tile t, as micro-steps of a few VALU ops placed
+// one per MFMA gap (sched_barrier-pinned) and ONE 16-B store per K-tile (v_permlane16_swap pairs the
+// two rows) instead of a burst: beside the DMA pieces a store costs its issue, not its bytes (two
+// 8-B stores per K-tile: 878 TF/s on c_fc-plain; the same without stores 1,284).
 //  * LDS: a 3-stage ring of 48-KB stages (A 256 x 64, W 128 x 64 bf16; 128-B rows, 16-B chunk c of
 //    row r at c ^ ((r >> 1) & 7)) + per wave two 1.5-KB side sets (bias, LN-fold column sums,
 //    (mu, rstd) of the tile's rows: LDS-DMA'd during the tile's K-tile 0, read by the next tile).
-//  * K-tile g: [set-0 MFMAs | set-1 reads | 6 DMA pieces of step g+2 | fragment EJ] -> wait for step
-//    g+1 -> barrier -> [set-1 MFMAs | set-0 reads of step g+1 | 6 DMA pieces | fragment EJ+1]: one
+//  * K-tile g: [set-0 MFMAs | set-1 reads | 6 DMA pieces of step g+2 | row 2 EP] -> wait for step
+//    g+1 -> barrier -> [set-1 MFMAs | set-0 reads of step g+1 | 6 DMA pieces | row 2 EP + 1, store]: one
 //    barrier per K-tile; step g+2 goes into the stage step g-1 used (free since the last barrier)
 //    and every wait's vmcnt is exact, stores included (the first tile's sub-chunks store through a
 //    0-row descriptor: dropped, still counted).
@@ -30,6 +32,7 @@ namespace {
 
 constexpr int BM = 256, BK = 64;
 using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
 
 __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
@@ -83,8 +86,7 @@ constexpr int DB_SIDE = 1536;                           // bias 256 B | fold_c 2
 
 // V: timing variants (GEMM variant bits 14..17): bit 0 = no sched_barrier pinning of the
 // micro-steps (the compiler schedules them); bit 1 = no sub-chunks at all (ablation: no output);
-// bit 2 = sub-chunks without their stores (ablation); bit 3 = both stores of a sub-chunk at the
-// end of the second half (two K-tiles to retire instead of one)
+// bit 2 = sub-chunks without their stores (ablation)
 template <int ACT, int EPI, int V = 0>
 __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
     constexpr bool FOLD = EPI == EPI_LN_FOLD;
@@ -224,7 +226,8 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
         int pso = (PAR ^ 1) * DB_SIDE;
         asm volatile("" : "+s"(pso));
         const char* psd = side0 + pso;
-        const int ovo = fr * (int)p.ldo * 2 + (pnb + 4 * fq) * 2;    // this lane's store offset
+        // this lane's store offset: row fr + 16 (fq & 1) of a fragment-row pair, columns 8 (fq >> 1) ..
+        const int ovo = ((fr + (fq & 1) * 16) * (int)p.ldo + pnb + (fq >> 1) * 8) * 2;
 
         auto ktile = [&](auto kc) __attribute__((always_inline)) {
             // KT 0..15: K-tile KT of the tile, carrying sub-chunk KT of the previous tile; -1: K-tile 16
@@ -241,13 +244,13 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
             const char* sn = smem + bn;
             const int st2 = st == 0 ? 2 : st - 1;               // (g + 2) % 3
             const bool live = g + 2 < nsteps;
-            // sub-chunk KT: fragment row EI, column fragments EJ (first half) and EJ + 1 (second half),
+            // sub-chunk KT: fragment rows 2 EP (first half) and 2 EP + 1 (second half), column EJ,
             // each as 18 micro-steps of <= 4 VALU ops placed one per MFMA (sched_barrier-pinned):
             // one wave per SIMD issues them in the shadow of its own MFMAs
-            constexpr int EI = SUB ? (KT >> 1) : 0;
-            constexpr int EJ = SUB ? 2 * (KT & 1) : 0;
-            float4 ebv[2], ecv[2];
-            float2 esv;
+            constexpr int EP = SUB ? (KT >> 2) : 0;          // fragment rows 2 EP (first half), 2 EP + 1
+            constexpr int EJ = SUB ? (KT & 3) : 0;           // column fragment
+            float4 ebv[1], ecv[1];
+            float2 esv[2];
             f32x4 ex[2], eu[2], ew[2], ez[2], ed[2];
             float eq0[2], eq1[2];
             u32x2 eo[2];
@@ -256,22 +259,22 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
                 constexpr bool GL = ACT == ACT_GELU;
                 f32x4& x = ex[H];
                 if constexpr (K == 0) {
-                    x = accP[EI][EJ + H];
+                    x = accP[2 * EP + H][EJ];
                 } else if constexpr (K == 1) {
                     if constexpr (FOLD) {
-                        const float c[4] = {ecv[H].x, ecv[H].y, ecv[H].z, ecv[H].w};
+                        const float c[4] = {ecv[0].x, ecv[0].y, ecv[0].z, ecv[0].w};
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) x[e] = fmaf(-esv.x, c[e], x[e]);
+                        for (int e = 0; e < 4; ++e) x[e] = fmaf(-esv[H].x, c[e], x[e]);
                     } else {
-                        const float b[4] = {ebv[H].x, ebv[H].y, ebv[H].z, ebv[H].w};
+                        const float b[4] = {ebv[0].x, ebv[0].y, ebv[0].z, ebv[0].w};
 #pragma unroll
                         for (int e = 0; e < 4; ++e) x[e] += b[e];
                     }
                 } else if constexpr (K == 2) {
                     if constexpr (FOLD) {
-                        const float b[4] = {ebv[H].x, ebv[H].y, ebv[H].z, ebv[H].w};
+                        const float b[4] = {ebv[0].x, ebv[0].y, ebv[0].z, ebv[0].w};
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) x[e] = fmaf(esv.y, x[e], b[e]);
+                        for (int e = 0; e < 4; ++e) x[e] = fmaf(esv[H].y, x[e], b[e]);
                     }
                     if constexpr (!GL && ACT != ACT_NONE) {
 #pragma unroll
@@ -318,11 +321,16 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
                     for (int e = 0; e < 4; ++e) x[e] *= ew[H][e];
                 } else if constexpr (K == 16) {
                     eo[H] = u32x2{pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3])};
-                } else if constexpr (K == 17) {
-                    // one lane offset per tile, the fragment's row / column step in soffset
-                    int so = 16 * EI * (int)p.ldo * 2 + 32 * (EJ + H);
+                } else if constexpr (K == 17 && H == 1) {
+                    // rows 2 EP and 2 EP + 1 paired by v_permlane16_swap: each lane stores 8 columns of
+                    // one row (16 B), one store instruction per sub-chunk (a wave's store issue is
+                    // the cost beside the DMAs, not its bytes); row / column step in soffset
+                    const auto px = __builtin_amdgcn_permlane16_swap(eo[0][0], eo[1][0], false, false);
+                    const auto py = __builtin_amdgcn_permlane16_swap(eo[0][1], eo[1][1], false, false);
+                    const u32x4 d = {px[0], py[0], px[1], py[1]};
+                    int so = 32 * EP * (int)p.ldo * 2 + 32 * EJ;
                     asm volatile("" : "+s"(so));
-                    __builtin_amdgcn_raw_buffer_store_b64(eo[H], osrd, ovo, so, 0);
+                    if constexpr ((V & 4) == 0) __builtin_amdgcn_raw_buffer_store_b128(d, osrd, ovo, so, 0);
                 }
             };
             // ---- first half: set-0 MFMAs, set-1 reads, column fragment EJ of the sub-chunk ----
@@ -347,19 +355,17 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
                         // which would drain every store and DMA; retired by the lgkmcnt(2) at slot 3
                         const unsigned cb = (unsigned)(uintptr_t)(CE_LDS const void*)psd + (4 * fq) * 4;
                         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ebv[0]) : "v"(cb), "n"(64 * EJ));
-                        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ebv[1]) : "v"(cb), "n"(64 * EJ + 64));
                         if constexpr (FOLD) {
                             const unsigned sa = (unsigned)(uintptr_t)(CE_LDS const void*)psd + fr * 8;
                             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ecv[0]) : "v"(cb), "n"(256 + 64 * EJ));
-                            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ecv[1]) : "v"(cb), "n"(256 + 64 * EJ + 64));
-                            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(esv) : "v"(sa), "n"(512 + 128 * EI));
+                            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(esv[0]) : "v"(sa), "n"(512 + 256 * EP));
+                            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(esv[1]) : "v"(sa), "n"(512 + 256 * EP + 128));
                         }
                     }
                     // the side reads are older than the set-1 reads of slots 1 and 3
                     if (s2 == 3) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
                     if constexpr (s2 >= 2 && s2 <= 18)
                         estep(std::integral_constant<int, s2 - 2>{}, std::integral_constant<int, 0>{});
-                    if constexpr (s2 == 19 && (V & 12) == 0) estep(std::integral_constant<int, 17>{}, std::integral_constant<int, 0>{});
                 }
             });
             if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
             // leaves it open: a longer wait, never a short one)
             {
                 // C1 / C2: stores of a sub-chunk in its first / second half
-                constexpr int C1 = (V & 14) ? 0 : 1, C2 = (V & 6) ? 0 : (V & 8) ? 2 : 1;
+                constexpr int C1 = 0, C2 = (V & 6) ? 0 : 1;
                 constexpr int CNT = 6 + (KT == 0 ? NSIDE : 0) + (KT >= 1 || KT == -1 ? C2 : 0) + (KT >= 0 ? C1 : 0);
                 asm volatile("s_waitcnt vmcnt(%0)" :: "n"(CNT) : "memory");
             }
@@ -390,8 +396,7 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
                 }
                 if constexpr (SUB) {
                     if constexpr (s2 <= 16) estep(std::integral_constant<int, s2>{}, std::integral_constant<int, 1>{});
-                    if constexpr (s2 == 30 && (V & 8)) estep(std::integral_constant<int, 17>{}, std::integral_constant<int, 0>{});
-                    if constexpr (s2 == 31 && (V & 4) == 0) estep(std::integral_constant<int, 17>{}, std::integral_constant<int, 1>{});
+                    if constexpr (s2 == 31) estep(std::integral_constant<int, 17>{}, std::integral_constant<int, 1>{});
                 }
             });
             if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
@@ -467,7 +472,6 @@ hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipSt
         if (v == 1) hipLaunchKernelGGL((gemm_db<A_, E_, 1>), g, b, 0, s, p); \
         else if (v == 2) hipLaunchKernelGGL((gemm_db<A_, E_, 2>), g, b, 0, s, p); \
         else if (v == 4) hipLaunchKernelGGL((gemm_db<A_, E_, 4>), g, b, 0, s, p); \
-        else if (v == 8) hipLaunchKernelGGL((gemm_db<A_, E_, 8>), g, b, 0, s, p); \
         else hipLaunchKernelGGL((gemm_db<A_, E_>), g, b, 0, s, p); \
         return hipGetLastError(); }
     CE_DB(ACT_NONE, EPI_PLAIN) CE_DB(ACT_GELU, EPI_PLAIN) CE_DB(ACT_QGELU, EPI_PLAIN)
