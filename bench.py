@@ -210,7 +210,8 @@ def build_clip(args, dev, rank, world):
     return dict(engine=model.engine, step=step, pairs=B, flops_per_pair=FLOPS_PER_PAIR, sd=sd, cfg=cfg,
                 flops_exec_per_pair=FLOPS_PER_PAIR - pi - pt,
                 # profiles/pmc_traffic.json was measured on this default configuration
-                pmc_config=(B == 256 and not args.no_pooled_prune),
+                pmc_tags=("gemm_fc_v", "gemm_qkv_v", "attn_v")
+                if B == 256 and not args.no_pooled_prune else (),
                 metric="image-text pairs/sec ViT-L/14-336", config=cfgd)
 
 
@@ -249,6 +250,8 @@ def build_pacl(args, dev, rank, world):
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
                 flops_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops,
                 flops_exec_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops - pt,
+                # profiles/pmc_traffic.json's pacl_pool entry was measured on this default configuration
+                pmc_tags=("pacl_pool",) if B == 512 and args.pacl_mode == "ones" else (),
                 metric="PACL image-text pairs/sec ViT-L/14-336", config=cfgd, hbm_kernel="pacl_pool")
 
 
@@ -462,14 +465,14 @@ def main():
             ach = (top["flops"] / top["launches"]) / (per_ms * 1e-3) / 1e12
             roof = {"bound": "mfma", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                    "traffic": load_traffic(top["name"]) if W.get("pmc_config") else None,
+                    "traffic": load_traffic(top["name"]) if top["name"] in W.get("pmc_tags", ()) else None,
                     "avg_launch_ms": round(per_ms, 4),
                     "flops_per_launch": top["flops"] / top["launches"]}
         else:
             ach = (top["bytes"] / top["launches"]) / (per_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                    "traffic": load_traffic(top["name"]) if W.get("pmc_config") else None}
+                    "traffic": load_traffic(top["name"]) if top["name"] in W.get("pmc_tags", ()) else None}
         # executed FLOPs (the pooled-only prune skips part of the last blocks) and the reference
         # model's FLOPs per pair (open_clip's profile), both over the dense bf16 peak
         fx = W.get("flops_exec_per_pair", W["flops_per_pair"])
@@ -484,7 +487,8 @@ def main():
                 gbs = (s["bytes"] / s["launches"]) / (per * 1e-3) / 1e9
                 roof["hbm_kernel"] = {"kernel": hk, "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                       "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": round(per, 4),
-                                      "bytes_per_launch": s["bytes"] / s["launches"]}
+                                      "bytes_per_launch": s["bytes"] / s["launches"],
+                                      "traffic": load_traffic(hk) if hk in W.get("pmc_tags", ()) else None}
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline and args.workload == "clip":

@@ -14,10 +14,13 @@ import os
 import sys
 from collections import defaultdict
 
-# bench tag -> (kernel-name prefix, grid size in threads) of the image tower at B = 256
+# bench tag -> (kernel-name prefix(es), grid size in threads) of the image tower at B = 256 (clip
+# workload) and of the PACL pooling at B = 512 (pacl workload: its two passes sum to one launch)
 TAGS = {"gemm_fc_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<1, false, true, 2", 65536),
         "gemm_qkv_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<0, false, true, 2", 65536),
-        "attn_v": ("void ce::(anonymous namespace)::attn_fwd<false", None)}
+        "attn_v": ("void ce::(anonymous namespace)::attn_fwd<false", None),
+        "pacl_pool": (("void ce::(anonymous namespace)::pacl_pool_part_k", "ce::(anonymous namespace)::pacl_pool_finish_k"),
+                      None)}
 
 
 def load(d, counter):
@@ -44,14 +47,24 @@ def main():
     if os.path.exists(out):
         with open(out) as f:
             res = json.load(f)
-    for tag, (pref, grid) in TAGS.items():
-        fs = [v for (k, g), vs in fetch.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
-        ws = [v for (k, g), vs in write.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
-        if not fs or not ws:
+    for tag, (prefs, grid) in TAGS.items():
+        prefs = prefs if isinstance(prefs, tuple) else (prefs,)
+        f2 = wr = 0.0
+        n = []
+        for pref in prefs:
+            fs = [v for (k, g), vs in fetch.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
+            ws = [v for (k, g), vs in write.items() if k.startswith(pref) and (grid is None or g == grid) for v in vs]
+            if not fs or not ws:
+                break
+            f2 += 2 * sum(fs) / len(fs) * 1024
+            wr += sum(ws) / len(ws) * 1024
+            n += [len(fs), len(ws)]
+        else:
+            pass
+        if len(n) != 2 * len(prefs):
             continue
-        f2, wr = 2 * sum(fs) / len(fs) * 1024, sum(ws) / len(ws) * 1024
         res[tag] = {"hbm_bytes_per_launch": round(f2 + wr), "fetch_bytes_corrected": round(f2),
-                    "write_bytes": round(wr), "dispatches": [len(fs), len(ws)],
+                    "write_bytes": round(wr), "dispatches": n,
                     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over bench.py, {fd}, {wd}"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
