@@ -477,12 +477,48 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_k(float2* __restrict__ 
     if (live && k0 == 0) stats[r] = make_float2(mu, rsqrtf(m2 / (64.0f * nslab) + 1e-5f));
 }
 
+// The same for an even nslab <= 16 (D = 1024 / 768): 8 lanes per row, lane k holding slabs 2k and
+// 2k + 1 (one 16-B load), two rows 32 apart per lane, so every lane has two loads in flight (the
+// one-8-B-load-per-lane form above was latency-bound: 71 % of its wave cycles parked in s_waitcnt)
+__global__ __launch_bounds__(256) void ln_stats_finalize16_k(float2* __restrict__ stats, const float2* __restrict__ part,
+                                                             int rows, int nslab, const int* __restrict__ m_dev) {
+    if (m_dev) rows = min(rows, *m_dev);
+    const int k0 = threadIdx.x & 7;
+    const int rb = blockIdx.x * 64 + (threadIdx.x >> 3);
+    const bool has = 2 * k0 < nslab;
+    float4 v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int r = rb + 32 * u;
+        v[u] = (r < rows && has) ? *reinterpret_cast<const float4*>(part + (size_t)r * nslab + 2 * k0)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float sm = v[u].x + v[u].z;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const float mu = sm / (float)nslab;
+        const float d0 = v[u].x - mu, d1 = v[u].z - mu;
+        float m2 = has ? (v[u].y + 64.0f * d0 * d0) + (v[u].w + 64.0f * d1 * d1) : 0.f;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+        const int r = rb + 32 * u;
+        if (r < rows && k0 == 0) stats[r] = make_float2(mu, rsqrtf(m2 / (64.0f * nslab) + 1e-5f));
+    }
+}
+
 }  // namespace
 
 hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s,
                                     const int* m_dev) {
     if (rows <= 0) return hipSuccess;
     if (nslab <= 0 || nslab > 64) return hipErrorInvalidValue;
+    if (nslab <= 16 && nslab % 2 == 0 && ((uintptr_t)part & 15) == 0) {
+        hipLaunchKernelGGL(ln_stats_finalize16_k, dim3((unsigned)((rows + 63) / 64)), dim3(256), 0, s, stats, part,
+                           rows, nslab, m_dev);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(ln_stats_finalize_k, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, stats, part, rows,
                        nslab, m_dev);
     return hipGetLastError();
