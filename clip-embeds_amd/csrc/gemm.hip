@@ -140,7 +140,10 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        GEMM_VAR_W4_SPREAD_EVEN = 4096,
        // honour GemmParams::onetile: the caller's small grids (text tower) on the four-wave kernels
        // with one tile per workgroup instead of the 8-wave 4-phase kernel
-       GEMM_VAR_SMALL_ONETILE = 8192 };
+       GEMM_VAR_SMALL_ONETILE = 8192,
+       // (bits 14..17: SCHED 13 timing variants, gemm_db.hip)
+       // the staged-residual kernel drains every epilogue store before the next tile's K-loop
+       GEMM_VAR_RHL_DRAIN = 1 << 18 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \
@@ -2216,6 +2219,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, stb[sl]), ss, so + 64 * ns * 8 + sl * 8, 0, 0);
             }
         }
+        // ABL bit 3 (GEMM_VAR_RHL_DRAIN): every store of this epilogue retires here, so none is in
+        // flight beside the next tile's K-loop DMAs (whose waits would otherwise cover them)
+        if constexpr ((ABL & 8) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         trace_stamp(p, 2, t * grid + blockIdx.x);
     }
 #undef CE_MFMA_AGPR
@@ -2633,7 +2639,9 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.stagger = gemm_stagger();
             plan_tail_rhl(p, nwg, w4pp_grid(nwg, p.onetile));
             const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
-            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
+            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && (gemm_variant() & GEMM_VAR_RHL_DRAIN))
+                hipLaunchKernelGGL(gemm_w4_resid_hl<12>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
                 hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
             else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
             else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
