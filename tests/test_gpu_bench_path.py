@@ -276,3 +276,22 @@ def test_pacl_batch512_golden_rows(golden, tag):
     assert cos_dist(b[[0, 511]], g[f"{tag}_txt"]) < COS_TOL
     assert np.isfinite(a).all() and np.isfinite(b).all()
     np.testing.assert_allclose(np.linalg.norm(a, axis=-1), 1.0, rtol=1e-4)
+
+
+@pytest.mark.parametrize("rows,ns", [(147712, 16), (19713, 12), (1000, 9), (65, 16), (3, 2)])
+def test_ln_stats_finalize_kernels(rows, ns):
+    """(mu, rstd) from 64-column slab (mean, M2) partials: the two-row 16-B-load kernel (even ns <= 16:
+    D = 1024 / 768) and the 16-lane kernel (odd ns), ragged row counts, vs torch f32 from the same
+    partials (Chan's combine of equal-count slabs)."""
+    g = torch.Generator(device="cpu").manual_seed(rows + ns)
+    x = (torch.randn(rows, ns, 64, generator=g) * torch.rand(rows, 1, 1, generator=g) * 3 + 0.5).to(DEV)
+    part = torch.stack([x.mean(-1), ((x - x.mean(-1, keepdim=True)) ** 2).sum(-1)], -1).contiguous()
+    stats = torch.full((rows + 8, 2), 7.0, device=DEV)
+    _lib.call("ce_kernel_ln_stats_finalize", S(), P(stats), P(part), rows, ns)
+    torch.cuda.synchronize()
+    xf = x.reshape(rows, ns * 64)
+    mu = xf.mean(-1)
+    rstd = torch.rsqrt(xf.var(-1, unbiased=False) + 1e-5)
+    np.testing.assert_allclose(stats[:rows, 0].cpu().numpy(), mu.cpu().numpy(), atol=1e-5)
+    np.testing.assert_allclose(stats[:rows, 1].cpu().numpy(), rstd.cpu().numpy(), rtol=1e-4)
+    assert bool((stats[rows:] == 7.0).all())
