@@ -85,8 +85,9 @@ constexpr int DB_STAGE = DB_A_BYTES + DB_BN * BK * 2;   // 48 KB
 constexpr int DB_SIDE = 1536;                           // bias 256 B | fold_c 256 B | (mu, rstd) 1 KB
 
 // V: timing variants (GEMM variant bits 14..17): bit 0 = no sched_barrier pinning of the
-// micro-steps (the compiler schedules them); bit 1 = no sub-chunks at all (ablation: no output);
-// bit 2 = sub-chunks without their stores (ablation)
+// micro-steps (the compiler schedules them; measured equal to the pinned form, no longer
+// instantiated); bit 1 = no sub-chunks at all (ablation: no output); bit 2 = sub-chunks without
+// their stores (ablation)
 template <int ACT, int EPI, int V = 0>
 __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
     constexpr bool FOLD = EPI == EPI_LN_FOLD;
@@ -469,8 +470,7 @@ hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipSt
     const int v = ((p.variant >> 14) & 15);
 #define CE_DB(A_, E_) \
     if (act == A_ && epi == E_) { \
-        if (v == 1) hipLaunchKernelGGL((gemm_db<A_, E_, 1>), g, b, 0, s, p); \
-        else if (v == 2) hipLaunchKernelGGL((gemm_db<A_, E_, 2>), g, b, 0, s, p); \
+        if (v == 2) hipLaunchKernelGGL((gemm_db<A_, E_, 2>), g, b, 0, s, p); \
         else if (v == 4) hipLaunchKernelGGL((gemm_db<A_, E_, 4>), g, b, 0, s, p); \
         else hipLaunchKernelGGL((gemm_db<A_, E_>), g, b, 0, s, p); \
         return hipGetLastError(); }
