@@ -141,9 +141,9 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        // honour GemmParams::onetile: the caller's small grids (text tower) on the four-wave kernels
        // with one tile per workgroup instead of the 8-wave 4-phase kernel
        GEMM_VAR_SMALL_ONETILE = 8192,
-       // (bits 14..17: SCHED 13 timing variants, gemm_db.hip)
+       // (bits 14..18: SCHED 13 timing variants, gemm_db.hip)
        // the staged-residual kernel drains every epilogue store before the next tile's K-loop
-       GEMM_VAR_RHL_DRAIN = 1 << 18 };
+       GEMM_VAR_RHL_DRAIN = 1 << 19 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \

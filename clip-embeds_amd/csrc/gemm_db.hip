@@ -87,7 +87,8 @@ constexpr int DB_SIDE = 1536;                           // bias 256 B | fold_c 2
 // V: timing variants (GEMM variant bits 14..17): bit 0 = no sched_barrier pinning of the
 // micro-steps (the compiler schedules them; measured equal to the pinned form, no longer
 // instantiated); bit 1 = no sub-chunks at all (ablation: no output); bit 2 = sub-chunks without
-// their stores (ablation)
+// their stores (ablation); bit 3 = stores through a 0-record descriptor (issued, dropped); bit 4 =
+// non-temporal stores
 template <int ACT, int EPI, int V = 0>
 __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
     constexpr bool FOLD = EPI == EPI_LN_FOLD;
@@ -331,7 +332,14 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
                     const u32x4 d = {px[0], py[0], px[1], py[1]};
                     int so = 32 * EP * (int)p.ldo * 2 + 32 * EJ;
                     asm volatile("" : "+s"(so));
-                    if constexpr ((V & 4) == 0) __builtin_amdgcn_raw_buffer_store_b128(d, osrd, ovo, so, 0);
+                    // (timing variants: V bit 3 stores through a 0-record descriptor, dropped after issue;
+                    // V bit 4 stores with the non-temporal policy)
+                    if constexpr ((V & 4) == 0 && (V & 8) == 0 && (V & 16) == 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(d, osrd, ovo, so, 0);
+                    else if constexpr ((V & 8) != 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(d, make_srd(p.out, 0), ovo, so, 0);
+                    else if constexpr ((V & 16) != 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(d, osrd, ovo, so, 2);
                 }
             };
             // ---- first half: set-0 MFMAs, set-1 reads, column fragment EJ of the sub-chunk ----
@@ -467,11 +475,13 @@ __global__ __launch_bounds__(256, 1) void gemm_db(GemmParams p) {
 
 hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipStream_t s) {
     const dim3 g((unsigned)grid), b(256);
-    const int v = ((p.variant >> 14) & 15);
+    const int v = ((p.variant >> 14) & 31);
 #define CE_DB(A_, E_) \
     if (act == A_ && epi == E_) { \
         if (v == 2) hipLaunchKernelGGL((gemm_db<A_, E_, 2>), g, b, 0, s, p); \
         else if (v == 4) hipLaunchKernelGGL((gemm_db<A_, E_, 4>), g, b, 0, s, p); \
+        else if (v == 8) hipLaunchKernelGGL((gemm_db<A_, E_, 8>), g, b, 0, s, p); \
+        else if (v == 16) hipLaunchKernelGGL((gemm_db<A_, E_, 16>), g, b, 0, s, p); \
         else hipLaunchKernelGGL((gemm_db<A_, E_>), g, b, 0, s, p); \
         return hipGetLastError(); }
     CE_DB(ACT_NONE, EPI_PLAIN) CE_DB(ACT_GELU, EPI_PLAIN) CE_DB(ACT_QGELU, EPI_PLAIN)
