@@ -285,9 +285,14 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int D = H * 64, ld = 3 * D;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // zero the transposed / P / dS images (their contraction padding must read as 0)
-    for (int e = tid; e < (3 * 64 * AB_LT + 3 * AB_L * AB_LT) / 8; e += 256)
-        reinterpret_cast<uint4*>(QT)[e] = make_uint4(0, 0, 0, 0);
+    // zero the contraction padding of the transposed / P / dS images: columns 16 nt .. AB_KP - 1 of
+    // their 3 x 64 + 3 x 80 rows (every column below 16 nt is written below: zero rows for i >= L,
+    // p = dS = 0 for masked entries of the nt x nt score tiles); 16-B chunks
+    {
+        const int c0 = ((L + 15) / 16) * 16, nch = (AB_KP - c0) / 8;
+        for (int e = tid; e < (3 * 64 + 3 * AB_L) * nch; e += 256)
+            *reinterpret_cast<uint4*>(QT + (e / nch) * AB_LT + c0 + (e % nch) * 8) = make_uint4(0, 0, 0, 0);
+    }
     if (tid < AB_L) lrow[tid] = tid < L ? lse[(size_t)bh * L + tid] : 0.f;
     __syncthreads();
     // load q', k, v, dO rows (16 B per thread-chunk) + delta_i = dO_i . O_i
