@@ -75,7 +75,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                                                     bf16_t* __restrict__ out, int Lp, int H,
                                                     float qscale, float* __restrict__ lse,
                                                     const int* __restrict__ seg) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    constexpr bool RING3 = (VAR & 128) != 0;  // three K/V slots: tile t+2 in flight beside t+1 (ONEBAR)
+    __shared__ __attribute__((aligned(16))) char smem[(RING3 ? 3 : 2) * STAGE_BYTES];
     constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
     constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
@@ -291,11 +292,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     };
 
     stage(0, 0);
-    // one key tile; BUF (the ring slot, t & 1) is a compile-time constant so every LDS address
-    // is a per-lane offset plus an immediate (the loop is unrolled by two)
+    if constexpr (RING3) {
+        if (nkt > 1) stage(1, 1);
+    }
+    // one key tile; BUF (the ring slot, t & 1, or t % 3 with RING3) is a compile-time constant so
+    // every LDS address is a per-lane offset plus an immediate (the loop is unrolled by two / three)
     auto tile = [&](const int t, auto bufc) {
         constexpr int BUF = decltype(bufc)::value;
-        if (ONEBAR) {
+        if constexpr (RING3) {
+            // tile t landed (tile t+1's 4 DMAs may stay in flight) and every wave is done with tile
+            // t-1, whose slot (t+2) % 3 then takes tile t+2
+            if (t + 1 < nkt) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            barrier();
+            if (t + 2 < nkt) stage(t + 2, (BUF + 2) % 3);
+        } else if (ONEBAR) {
             // tile t landed (the only DMA in flight) and every wave is done with tile t-1, whose
             // slot BUF^1 then takes tile t+1
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -463,9 +474,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             barrier();
         }
     };
-    for (int t = 0; t < nkt; t += 2) {
-        tile(t, std::integral_constant<int, 0>{});
-        if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
+    if constexpr (RING3) {
+        for (int t = 0; t < nkt; t += 3) {
+            tile(t, std::integral_constant<int, 0>{});
+            if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
+            if (t + 2 < nkt) tile(t + 2, std::integral_constant<int, 2>{});
+        }
+    } else {
+        for (int t = 0; t < nkt; t += 2) {
+            tile(t, std::integral_constant<int, 0>{});
+            if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
+        }
     }
 
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
@@ -663,6 +682,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     } else {
         switch (v) {
             case 125: CE_ATTN_LAUNCH(false, 125); break;
+            case 253: CE_ATTN_LAUNCH(false, 253); break;
             case 61: CE_ATTN_LAUNCH(false, 61); break;
             case 29: CE_ATTN_LAUNCH(false, 29); break;
             case 16: CE_ATTN_LAUNCH(false, 16); break;
@@ -682,7 +702,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61 || var == 125)
+                  var == 61 || var == 125 || var == 253)
                      ? var : 125;
     return prev;
 }
