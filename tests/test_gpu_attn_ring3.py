@@ -1,0 +1,31 @@
+"""Attention variant 253 (bit 128: three K/V LDS slots, tile t+2's DMA in flight beside tile t+1's)
+vs the default variant 125 and the f32 reference, on the shapes of the image tower (L = 577, ragged
+last key tile), a short sequence and the dominant-key / wide-score cases."""
+import pytest
+import torch
+
+from clipembed import _lib
+from test_gpu_kernels import attn_ref, run_attn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("B,L,H,scale", [(2, 577, 4, 1.0), (3, 577, 2, 3.0), (2, 65, 4, 1.0), (1, 1, 2, 1.0),
+                                         (2, 200, 3, 4.5)])
+def test_attention_ring3(B, L, H, scale):
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    L_ = _lib.lib()
+    outs = {}
+    for var in (253, 125):
+        prev = L_.ce_set_attn_variant(var)
+        try:
+            outs[var] = run_attn(qkv, B, L, H, False).float()
+        finally:
+            L_.ce_set_attn_variant(prev)
+    ref = attn_ref(qkv, B, L, H, False)
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    assert (outs[253] - ref).abs().max().item() < tol
+    # same arithmetic, only the K/V staging differs: bit-identical to the default variant
+    assert torch.equal(outs[253], outs[125])
