@@ -12,12 +12,17 @@ Workloads (BASELINE.json configs; a "step" is one pass of the hot path over one 
            contrastive logits [B, N*B] both ways (loss.py:137-164, local_loss).
   pacl     (configs[2]) PACL forward of B = 512 pairs per GPU (open_clip_pacl.forward, pacl.py:135-145:
            text tower + head, vision tower + patch head, fused patch alignment/pooling) + the PACL
-           ClipLoss (pacl.py:489-514; N > 1: all-gathered features, local logits).
+           ClipLoss(0.1) (pacl.py:489-514; N > 1: RCCL all-gather of the pooled features, each rank's
+           rows of the global logits, all-reduce of the CE sums: the value over the whole global batch,
+           as train_pacl.py:34-36 computes it after nn.DataParallel's gather).
   negclip  (configs[3]) NegCLIP training step, locked image tower: 1024 pairs + 512 hard-negative
            captions per GPU, text tower backward, RCCL all-reduce of text gradients, AdamW.
   sparc    (configs[4]) SPARC with precomputed text-token embeddings [B,77,768] + mask: image
            tower + patch head, patch x token similarity / alignment (pacl.py:455-478) and SparcLoss
-           (pacl.py:516-584; N > 1: global term over all-gathered means) for B = 256 per GPU.
+           (pacl.py:516-584, temperature 0.1 as train_sparc.py:105; N > 1: RCCL all-gather of the
+           [B,768] normalised patch / token means for the global term, the per-sample local term's sums
+           and the global CE sums all-reduced: the loss over the whole global batch, as
+           train_sparc.py:93,105 computes it after nn.DataParallel's gather) for B = 256 per GPU.
 
 Prints ONE JSON line (rank 0).  value = image-text pairs/s over all ranks (weak scaling: B pairs
 per GPU per step), inputs resident in HBM before the timed region.  `roofline` reports the
@@ -84,9 +89,10 @@ def host_cores():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(sd, cfg, batch=8, reps=3):
-    """The reference's f32 CPU forward (encode_image + encode_text + logits) at `batch` pairs, median
-    of `reps`, at the host core share and at 8 threads."""
+def cpu_baseline(sd, cfg, batch=8, reps=3, warmup=3):
+    """The reference's f32 CPU forward (encode_image + encode_text + logits) at `batch` pairs, `warmup`
+    untimed iterations then the median of `reps`, at the host core share and at 8 threads (SURVEY
+    §8(d))."""
     from oracle.clip_torch_cpu import TorchCLIP
     from clipembed import weights as W
     m = TorchCLIP(sd, cfg)
@@ -97,19 +103,19 @@ def cpu_baseline(sd, cfg, batch=8, reps=3):
     cores = host_cores()
     for n in sorted({cores, 8}, reverse=True):
         torch.set_num_threads(n)
-        m.encode_image(imgs[:1])                 # warm-up (thread pool, allocator)
         ts = []
-        for _ in range(reps):
+        for it in range(warmup + reps):
             t0 = time.perf_counter()
             fi = m.encode_image(imgs, normalize=True)
             ft = m.encode_text(caps, normalize=True)
             m.get_logits(fi, ft, 100.0)
-            ts.append(time.perf_counter() - t0)
+            if it >= warmup:
+                ts.append(time.perf_counter() - t0)
         res[n] = float(np.median(ts))
     torch.set_num_threads(prev)
     out = {"value": round(batch / res[cores], 4), "unit": "pairs/s", "cores": cores, "kind": "port",
-           "sample": f"{batch} image-text pairs per run, median of {reps}: full-depth ViT-L/14-336 f32 torch CPU "
-                     f"forward with the reference's ATen calls (oracle/clip_torch_cpu.py), encode_image + "
+           "sample": f"{batch} image-text pairs per run, {warmup} warm-up runs, median of {reps}: full-depth "
+                     f"ViT-L/14-336 f32 torch CPU forward with the reference's ATen calls (oracle/clip_torch_cpu.py), encode_image + "
                      f"encode_text + logits; {res[cores]:.2f} s at {cores} threads"}
     if 8 in res:
         out["value_8_threads"] = round(batch / res[8], 4)
@@ -218,7 +224,6 @@ def build_clip(args, dev, rank, world):
 def build_pacl(args, dev, rank, world):
     import clipembed
     from clipembed import weights as W
-    from clipembed.loss import ClipLoss as OpenClipLoss
     from clipembed.pacl import ClipLoss, open_clip_pacl, open_clip_pacl_rope_after
     cfg = clipembed.get_model_config("ViT-L-14-336")
     sd = W.synthetic_state_dict(cfg)
@@ -229,15 +234,12 @@ def build_pacl(args, dev, rank, world):
     B = args.batch or 512
     imgs = torch.from_numpy(W.synthetic_images(B, seed=1000 + rank)).to(dev)
     caps = torch.from_numpy(W.synthetic_captions(B, seed=2000 + rank)).to(dev)
-    loss = ClipLoss(0.1, engine=mod.engine)        # train_pacl.py: temperature 0.1
-    # N > 1: the PACL loss over all-gathered features as open_clip's ClipLoss(local_loss=True)
-    # (loss.py:137-193; tested on 2 gloo ranks in tests/test_dist_gloo.py)
-    dist_loss = OpenClipLoss(local_loss=True, rank=rank, world_size=world, engine=mod.engine)
+    # train_pacl.py:106: temperature 0.1; N > 1: the global-batch value from sharded rows (all-gather of
+    # the features + all-reduce of 5 floats; tests/test_dist_gloo.py, tests/test_gpu_dist_loss.py)
+    loss = ClipLoss(0.1, engine=mod.engine, rank=rank, world_size=world)
 
     def step():
         oi, ot = mod(imgs, caps)
-        if world > 1:
-            return dist_loss(oi, ot, loss.logit_scale)
         return loss(oi, ot)
 
     pool_flops = 2.0 * 576 * 768 * (2 if cls.weight_mode else 1)
@@ -245,7 +247,8 @@ def build_pacl(args, dev, rank, world):
                         "(BASELINE configs[2]: batch 512/GPU bf16)",
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
             "parallelism": f"dp{world}", "pacl_mode": args.pacl_mode,
-            "exchange": "RCCL all_gather of pooled embeddings" if world > 1 else "none"}
+            "exchange": ("RCCL all_gather of the pooled features [B,768] x2 + all_reduce of the loss's CE sums "
+                         "(global-batch ClipLoss value)") if world > 1 else "none"}
     _, pt = pooled_prune_flops(cfg, not args.no_pooled_prune, caps.cpu().numpy().argmax(1))  # pooled-only text
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
                 flops_per_pair=FLOPS_PER_PAIR + PACL_HEAD_FLOPS + pool_flops,
@@ -304,7 +307,7 @@ def build_sparc(args, dev, rank, world):
     l_tok = (torch.randn(B, T, D, generator=g) * 0.5).to(dev)
     eot = torch.randint(6, 42, (B,), generator=g)
     mask = (torch.arange(T).expand(B, -1) <= eot[:, None]).float().to(dev)
-    loss_fn = SparcLoss(0.07, engine=mod.engine)
+    loss_fn = SparcLoss(0.1, engine=mod.engine, rank=rank, world_size=world)     # train_sparc.py:105
 
     def step():
         v = mod.forward_visual(imgs)
@@ -315,7 +318,9 @@ def build_sparc(args, dev, rank, world):
     cfgd = {"workload": f"SPARC ({cls.__name__}) image tower + patch head, patch x token similarity / alignment, "
                         "SparcLoss with precomputed text-token embeddings (BASELINE configs[4]: batch 256/GPU)",
             "batch_per_gpu": B, "global_batch": world * B, "tokens": T, "patches": P, "dim": D,
-            "parallelism": f"dp{world}", "exchange": "none (per-GPU SparcLoss)"}
+            "parallelism": f"dp{world}", "loss_temperature": 0.1,
+            "exchange": ("RCCL all_gather of the normalised patch / token means [B,768] x2 + all_reduce of the "
+                         "5 loss partial sums (global-batch SparcLoss value)") if world > 1 else "none"}
     return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
                 flops_per_pair=IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D, prunable=False,
                 metric="SPARC image-text pairs/sec ViT-L/14-336", config=cfgd)

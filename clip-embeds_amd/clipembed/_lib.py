@@ -81,6 +81,13 @@ _SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p]),
     "ce_sparc_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                               c_int, c_float, c_float, c_float, c_void_p]),
+    "ce_sparc_loss_means": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                    c_void_p]),
+    "ce_sparc_loss_partial": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_int, c_int, c_int, c_float, c_void_p]),
+    "ce_contrastive_loss_partial": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                            c_float, c_void_p]),
+    "ce_loss_combine": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_void_p]),
     "ce_preprocess_images": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                      c_int, c_void_p]),
     "ce_preprocess_images_boxes": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -215,14 +215,39 @@ class sparc_rope(sparc):
     rope = _lib.CE_ROPE_BEFORE
 
 
+def _all_gather_rows(x: torch.Tensor, world_size: int) -> torch.Tensor:
+    """Every rank's [B, D] rows concatenated in rank order (torch.distributed: RCCL over xGMI with
+    the "nccl" backend; gloo in the CPU / single-GPU tests)."""
+    import torch.distributed as dist
+    parts = [torch.empty_like(x) for _ in range(world_size)]
+    dist.all_gather(parts, x.contiguous())
+    return torch.cat(parts, dim=0)
+
+
+def _all_reduce_sum(x: torch.Tensor) -> torch.Tensor:
+    import torch.distributed as dist
+    dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x
+
+
 class ClipLoss(torch.nn.Module):
     """PACL ClipLoss (pacl.py:486-514): logit_scale = 1 / temperature, labels arange, mean of the
-    image->text and text->image cross entropies.  Logits and CE run in libclipembed."""
+    image->text and text->image cross entropies.  Logits and CE run in libclipembed.
 
-    def __init__(self, temperature: float, engine=None):
+    rank / world_size (not in the reference's signature, whose callers are single-process): the
+    batch is sharded over data-parallel ranks, and the value is the reference's loss over the WHOLE
+    batch, as train_pacl.py:34-36,95 computes it after nn.DataParallel gathers every replica's
+    outputs to one device.  The ranks all-gather the [B, D] features (equal B per rank), each takes
+    the CE sums of its own rows of the global logits both ways (ce_contrastive_loss_partial), one
+    all-reduce adds them, ce_loss_combine divides by the global batch.  Every rank returns the same
+    value."""
+
+    def __init__(self, temperature: float, engine=None, rank: int = 0, world_size: int = 1):
         super().__init__()
         self.logit_scale = 1.0 / temperature
         self.engine = engine
+        self.rank = rank
+        self.world_size = world_size
 
     def _engine(self, t: torch.Tensor):
         return self.engine if self.engine is not None else kernel_engine(t.device)
@@ -247,9 +272,32 @@ class ClipLoss(torch.nn.Module):
                   _ptr(labels), _ptr(out))
         return out
 
+    # --- the engine calls of the sharded path (a CPU test double replaces them in tests/test_dist_gloo.py)
+    def _contrastive_parts(self, e, img_all, txt_all, row0, B):
+        parts = torch.empty(5, device=img_all.device, dtype=torch.float32)
+        _lib.call("ce_contrastive_loss_partial", e.h, _stream(e.device), _ptr(img_all), _ptr(txt_all),
+                  img_all.shape[0], row0, B, img_all.shape[1], float(self.logit_scale), _ptr(parts))
+        return parts
+
+    def _combine(self, e, parts, n_global, global_weight, local_weight):
+        out = torch.empty((), device=parts.device, dtype=torch.float32)
+        _lib.call("ce_loss_combine", e.h, _stream(e.device), _ptr(parts), n_global, float(global_weight),
+                  float(local_weight), _ptr(out))
+        return out
+
     @torch.no_grad()
     def forward(self, image_features, text_features):
         e = self._engine(image_features)
+        if self.world_size > 1:
+            a = image_features.float().contiguous()
+            b = text_features.float().contiguous()
+            B = a.shape[0]
+            if b.shape[0] != B:
+                raise ValueError(f"ClipLoss: {B} image rows but {b.shape[0]} text rows")
+            img_all = _all_gather_rows(a, self.world_size)
+            txt_all = _all_gather_rows(b, self.world_size)
+            parts = _all_reduce_sum(self._contrastive_parts(e, img_all, txt_all, self.rank * B, B))
+            return self._combine(e, parts, img_all.shape[0], 1.0, 0.0)
         lpi, lpt = self.get_logits(image_features, text_features)
         labels = self.get_ground_truth(image_features.device, lpi.shape[0])
         return (self._ce(e, lpi, labels) + self._ce(e, lpt, labels)) / 2
@@ -257,12 +305,34 @@ class ClipLoss(torch.nn.Module):
 
 class SparcLoss(ClipLoss):
     """SparcLoss (pacl.py:516-584): global_weight * CLIP loss of the normalised patch / token means
-    + local_weight * the mean of the two masked pairwise local losses — one ce_sparc_loss call."""
+    + local_weight * the mean of the two masked pairwise local losses — one ce_sparc_loss call.
 
-    def __init__(self, temperature: float, engine=None):
-        super().__init__(temperature, engine)
+    rank / world_size: the reference's global-batch value (train_sparc.py:93,105: nn.DataParallel
+    gathers the replicas' outputs, SparcLoss runs on the whole batch) from a batch sharded over
+    ranks: ce_sparc_loss_means -> all-gather of the [B, 768] normalised means -> each rank's rows of
+    the global CE both ways + its samples' masked local sums (ce_sparc_loss_partial) -> all-reduce of
+    the 5 partial sums -> ce_loss_combine.  The local term stays per sample; only its sums and the
+    mask count cross ranks.  Every rank returns the same value."""
+
+    def __init__(self, temperature: float, engine=None, rank: int = 0, world_size: int = 1):
+        super().__init__(temperature, engine, rank, world_size)
         self.global_weight = 0.5
         self.local_weight = 1.0
+
+    def _means(self, e, v, lt):
+        B, P, D = v.shape
+        gi = torch.empty(B, D, device=v.device, dtype=torch.float32)
+        gt = torch.empty_like(gi)
+        _lib.call("ce_sparc_loss_means", e.h, _stream(e.device), _ptr(v), _ptr(lt), B, P, lt.shape[1], D,
+                  _ptr(gi), _ptr(gt))
+        return gi, gt
+
+    def _sparc_parts(self, e, img_all, txt_all, row0, lt, g, m):
+        B, T, D = lt.shape
+        parts = torch.empty(5, device=lt.device, dtype=torch.float32)
+        _lib.call("ce_sparc_loss_partial", e.h, _stream(e.device), _ptr(img_all), _ptr(txt_all), img_all.shape[0],
+                  row0, _ptr(lt), _ptr(g), _ptr(m), B, T, D, 1.0 / float(self.logit_scale), _ptr(parts))
+        return parts
 
     @torch.no_grad()
     def forward(self, v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask):
@@ -276,6 +346,12 @@ class SparcLoss(ClipLoss):
         if lt.shape != (B, T, D) or g.shape != (B, T, D) or m.shape != (B, T):
             raise ValueError(f"SparcLoss: shape mismatch v {tuple(v.shape)} l {tuple(lt.shape)} "
                              f"g {tuple(g.shape)} mask {tuple(m.shape)}")
+        if self.world_size > 1:
+            gi, gt = self._means(e, v, lt)
+            img_all = _all_gather_rows(gi, self.world_size)
+            txt_all = _all_gather_rows(gt, self.world_size)
+            parts = _all_reduce_sum(self._sparc_parts(e, img_all, txt_all, self.rank * B, lt, g, m))
+            return self._combine(e, parts, img_all.shape[0], self.global_weight, self.local_weight)
         out = torch.empty((), device=v.device, dtype=torch.float32)
         _lib.call("ce_sparc_loss", e.h, _stream(e.device), _ptr(v), _ptr(lt), _ptr(g), _ptr(m), B, P, T, D,
                   1.0 / float(self.logit_scale), float(self.global_weight), float(self.local_weight), _ptr(out))

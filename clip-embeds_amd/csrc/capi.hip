@@ -743,12 +743,17 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
     const int D = c.text.width, L = c.context_length;
     // LN folding as in the image tower: every block's fold current, D a multiple of 64
     std::vector<FoldBlk> folds(c.text.layers);
-    bool use_fold = h->ln_fold && D % 64 == 0 && D / 64 <= 64 && c.text.layers > 0;
+    // (the embedding kernel that seeds the folded stream covers these widths; others run unfolded)
+    const bool embed_ok = D == 256 || D == 512 || D == 768 || D == 1024 || D == 1280;
+    bool use_fold = h->ln_fold && embed_ok && c.text.layers > 0;
     for (int i = 0; use_fold && i < c.text.layers; ++i)
         use_fold = fold_block(h, "transformer.resblocks." + std::to_string(i) + ".", folds[i]);
     // pooled rows only (no tokens wanted): the last block for the EOT rows alone, and every block on
     // the packed rows 0..EOT of each caption
-    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && L >= 3;
+    // packed rows need GEMM kernels that clip at the device row count: the default schedule's
+    // (SCHED 1 and its four-wave / staged-residual kernels); a pinned other schedule runs every row
+    const bool prune = out_pooled && !keep_tokens && use_fold && h->resid_hl && h->pooled_prune && L >= 3 &&
+                       ce::current_gemm_sched() == 1;
     const int* seg = prune ? w.seg : nullptr;
     if (prune) CE_TRY(check_launch(ce::launch_text_pack(w.rows, w.seg, ids, B, L, s), "text_pack"));
     else if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
@@ -1574,6 +1579,58 @@ int ce_sparc_forward(ce_handle* h, void* stream, const float* v, const float* l,
     return CE_OK;
 }
 
+namespace {
+
+// Rows [row0, row0 + B) of the global CLIP loss of ClipLoss.forward (pacl.py:498-512) both ways:
+// Li = scale img_all[row0..] txt_all^T, Lt = scale txt_all[row0..] img_all^T ([B, Bg] each), per-row CE
+// against labels arange + row0 into lr / lc.  One shard (B == Bg): one fused launch for both ways.
+int contrastive_rows(ce_handle* h, hipStream_t s, const float* img_all, const float* txt_all, int Bg, int row0, int B,
+                     int D, float scale, float* Li, float* Lt, float* lr, float* lc) {
+    ce::FGemmParams a{};
+    a.A = img_all + (size_t)row0 * D; a.lda = D; a.B = txt_all; a.ldb = D; a.C = Li; a.ldc = Bg;
+    a.M = B; a.N = Bg; a.K = D; a.batch = 1; a.alpha = scale;
+    if (B == Bg) { a.Ct = Lt; a.ldct = Bg; }
+    CE_TRY(check_launch(ce::launch_fgemm(a, true, s), "loss global logits"));
+    if (B != Bg) {
+        ce::FGemmParams b = a;
+        b.A = txt_all + (size_t)row0 * D; b.B = img_all; b.C = Lt;
+        CE_TRY(check_launch(ce::launch_fgemm(b, true, s), "loss global logits"));
+    }
+    CE_TRY(check_launch(ce::launch_ce_diag_rows(lr, Li, B, Bg, row0, s), "loss ce"));
+    return check_launch(ce::launch_ce_diag_rows(lc, Lt, B, Bg, row0, s), "loss ce");
+}
+
+// SparcLoss's masked pairwise local loss of B samples (pacl.py:522-556,575-580): S[b] = scale grouped[b]
+// l[b]^T, per-sample masked row / column CE sums into part[B][3]
+int sparc_local_part(ce_handle* h, hipStream_t s, const float* l_tokens, const float* grouped, const float* mask, int B,
+                     int T, int D, float scale, float* S, float* part) {
+    ce::FGemmParams c{};
+    c.A = grouped; c.lda = D; c.sA = (long)T * D;
+    c.B = l_tokens; c.ldb = D; c.sB = (long)T * D;
+    c.C = S; c.ldc = T; c.sC = (long)T * T;
+    c.M = T; c.N = T; c.K = D; c.batch = B; c.alpha = scale;
+    CE_TRY(timed(h, s, "sparc_loss_local", 2.0 * B * T * T * D, 4.0 * B * (2.0 * T * D + (double)T * T),
+                 [&] { return ce::launch_fgemm(c, true, s); }));
+    return check_launch(ce::launch_sparc_local(part, S, mask, B, T, s), "sparc_loss local");
+}
+
+int sparc_means(hipStream_t s, const float* v_patch, const float* l_tokens, int B, int P, int T, int D, float* gi,
+                float* gt) {
+    CE_TRY(check_launch(ce::launch_mean_mid(gi, v_patch, B, P, D, s), "sparc_loss mean"));
+    CE_TRY(check_launch(ce::launch_mean_mid(gt, l_tokens, B, T, D, s), "sparc_loss mean"));
+    CE_TRY(check_launch(ce::launch_l2norm(gi, gi, B, D, s), "sparc_loss normalize"));
+    return check_launch(ce::launch_l2norm(gt, gt, B, D, s), "sparc_loss normalize");
+}
+
+int check_shard(const char* fn, int Bg, int row0, int B, int D) {
+    if (B <= 0 || D <= 0 || Bg <= 0 || row0 < 0 || row0 + B > Bg)
+        return fail(CE_ERR_INVALID, "%s: shard rows [%d, %d) outside the global batch of %d (D %d)", fn, row0,
+                    row0 + B, Bg, D);
+    return CE_OK;
+}
+
+}  // namespace
+
 int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float* l_tokens, const float* grouped,
                   const float* mask, int B, int P, int T, int D, float temperature, float global_weight,
                   float local_weight, float* out_loss) {
@@ -1585,7 +1642,7 @@ int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float*
     hipStream_t s = (hipStream_t)stream;
     const float scale = 1.0f / temperature;   // ClipLoss.logit_scale (pacl.py:491-493)
     const size_t nGI = (size_t)B * D, nG = (size_t)B * B, nS = (size_t)B * T * T;
-    CE_TRY(ensure_tmp(h, (2 * nGI + 2 * nG + nS + 5 * (size_t)B) * 4));
+    CE_TRY(ensure_tmp(h, (2 * nGI + 2 * nG + nS + 5 * (size_t)B + 8) * 4));
     float* gi = (float*)h->tmp;
     float* gt = gi + nGI;
     float* G = gt + nGI;
@@ -1594,28 +1651,70 @@ int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float*
     float* lr = S + nS;
     float* lc = lr + B;
     float* part = lc + B;
-    // global: normalise the patch / token means, CLIP loss both ways (pacl.py:566-576)
-    CE_TRY(check_launch(ce::launch_mean_mid(gi, v_patch, B, P, D, s), "sparc_loss mean"));
-    CE_TRY(check_launch(ce::launch_mean_mid(gt, l_tokens, B, T, D, s), "sparc_loss mean"));
-    CE_TRY(check_launch(ce::launch_l2norm(gi, gi, B, D, s), "sparc_loss normalize"));
-    CE_TRY(check_launch(ce::launch_l2norm(gt, gt, B, D, s), "sparc_loss normalize"));
-    ce::FGemmParams a{};
-    a.A = gi; a.lda = D; a.B = gt; a.ldb = D; a.C = G; a.ldc = B;
-    a.M = B; a.N = B; a.K = D; a.batch = 1; a.alpha = scale; a.Ct = Gt; a.ldct = B;
-    CE_TRY(check_launch(ce::launch_fgemm(a, true, s), "sparc_loss global logits"));
-    CE_TRY(check_launch(ce::launch_ce_diag_rows(lr, G, B, B, s), "sparc_loss ce"));
-    CE_TRY(check_launch(ce::launch_ce_diag_rows(lc, Gt, B, B, s), "sparc_loss ce"));
-    // local: S[b] = scale * grouped[b] l[b]^T, masked CE over rows and columns (pacl.py:578-582)
-    ce::FGemmParams c{};
-    c.A = grouped; c.lda = D; c.sA = (long)T * D;
-    c.B = l_tokens; c.ldb = D; c.sB = (long)T * D;
-    c.C = S; c.ldc = T; c.sC = (long)T * T;
-    c.M = T; c.N = T; c.K = D; c.batch = B; c.alpha = scale;
-    CE_TRY(timed(h, s, "sparc_loss_local", 2.0 * B * T * T * D, 4.0 * B * (2.0 * T * D + (double)T * T),
-                 [&] { return ce::launch_fgemm(c, true, s); }));
-    CE_TRY(check_launch(ce::launch_sparc_local(part, S, mask, B, T, s), "sparc_loss local"));
-    return check_launch(ce::launch_sparc_loss_finish(out_loss, lr, lc, part, B, global_weight, local_weight, s),
-                        "sparc_loss finish");
+    float* parts = part + 3 * (size_t)B;
+    // the whole batch is one shard: global term over the B x B logits, local term, combine
+    CE_TRY(sparc_means(s, v_patch, l_tokens, B, P, T, D, gi, gt));
+    CE_TRY(contrastive_rows(h, s, gi, gt, B, 0, B, D, scale, G, Gt, lr, lc));
+    CE_TRY(sparc_local_part(h, s, l_tokens, grouped, mask, B, T, D, scale, S, part));
+    CE_TRY(check_launch(ce::launch_loss_parts(parts, lr, lc, B, part, B, s), "sparc_loss parts"));
+    return check_launch(ce::launch_loss_combine(out_loss, parts, B, global_weight, local_weight, s),
+                        "sparc_loss combine");
+}
+
+int ce_sparc_loss_means(ce_handle* h, void* stream, const float* v_patch, const float* l_tokens, int B, int P, int T,
+                        int D, float* out_img, float* out_txt) {
+    if (!h || !v_patch || !l_tokens || !out_img || !out_txt) return fail(CE_ERR_INVALID, "ce_sparc_loss_means: null argument");
+    if (B <= 0 || P <= 0 || T <= 0 || D <= 0) return fail(CE_ERR_INVALID, "ce_sparc_loss_means: bad sizes");
+    DeviceGuard g(h->device);
+    return sparc_means((hipStream_t)stream, v_patch, l_tokens, B, P, T, D, out_img, out_txt);
+}
+
+int ce_sparc_loss_partial(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg, int row0,
+                          const float* l_tokens, const float* grouped, const float* mask, int B, int T, int D,
+                          float temperature, float* parts) {
+    if (!h || !img_all || !txt_all || !l_tokens || !grouped || !mask || !parts)
+        return fail(CE_ERR_INVALID, "ce_sparc_loss_partial: null argument");
+    if (T <= 0 || !(temperature > 0.f)) return fail(CE_ERR_INVALID, "ce_sparc_loss_partial: bad sizes or temperature");
+    CE_TRY(check_shard("ce_sparc_loss_partial", Bg, row0, B, D));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const float scale = 1.0f / temperature;
+    const size_t nL = (size_t)B * Bg, nS = (size_t)B * T * T;
+    CE_TRY(ensure_tmp(h, (2 * nL + nS + 5 * (size_t)B) * 4));
+    float* Li = (float*)h->tmp;
+    float* Lt = Li + nL;
+    float* S = Lt + nL;
+    float* lr = S + nS;
+    float* lc = lr + B;
+    float* part = lc + B;
+    CE_TRY(contrastive_rows(h, s, img_all, txt_all, Bg, row0, B, D, scale, Li, Lt, lr, lc));
+    CE_TRY(sparc_local_part(h, s, l_tokens, grouped, mask, B, T, D, scale, S, part));
+    return check_launch(ce::launch_loss_parts(parts, lr, lc, B, part, B, s), "sparc_loss parts");
+}
+
+int ce_contrastive_loss_partial(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg,
+                                int row0, int B, int D, float scale, float* parts) {
+    if (!h || !img_all || !txt_all || !parts) return fail(CE_ERR_INVALID, "ce_contrastive_loss_partial: null argument");
+    CE_TRY(check_shard("ce_contrastive_loss_partial", Bg, row0, B, D));
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t nL = (size_t)B * Bg;
+    CE_TRY(ensure_tmp(h, (2 * nL + 2 * (size_t)B) * 4));
+    float* Li = (float*)h->tmp;
+    float* Lt = Li + nL;
+    float* lr = Lt + nL;
+    float* lc = lr + B;
+    CE_TRY(contrastive_rows(h, s, img_all, txt_all, Bg, row0, B, D, scale, Li, Lt, lr, lc));
+    return check_launch(ce::launch_loss_parts(parts, lr, lc, B, nullptr, 0, s), "contrastive parts");
+}
+
+int ce_loss_combine(ce_handle* h, void* stream, const float* parts, int n_global, float global_weight,
+                    float local_weight, float* out_loss) {
+    if (!h || !parts || !out_loss) return fail(CE_ERR_INVALID, "ce_loss_combine: null argument");
+    if (n_global <= 0) return fail(CE_ERR_INVALID, "ce_loss_combine: bad global batch %d", n_global);
+    DeviceGuard g(h->device);
+    return check_launch(ce::launch_loss_combine(out_loss, parts, n_global, global_weight, local_weight,
+                                                (hipStream_t)stream), "loss combine");
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -70,6 +70,7 @@ hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipSt
 hipError_t launch_ln_stats_finalize(float2* stats, const float2* part, int rows, int nslab, hipStream_t s,
                                     const int* m_dev = nullptr);
 int set_gemm_schedule(int v);   // returns previous
+int current_gemm_sched();       // the current main-loop schedule (1 = default)
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
 int set_gemm_variant(int bits);  // kernel-variant bits for A/B (GEMM_VAR_*); returns previous
 int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 QKV-shape -> SCHED 11, ...); returns previous
@@ -180,10 +181,15 @@ hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t 
 
 // SparcLoss pieces (pacl.py:516-584)
 hipError_t launch_mean_mid(float* out, const float* x, int B, int P, int D, hipStream_t s);   // mean over dim 1
-hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, hipStream_t s);     // per-row CE vs arange
+// per-row CE vs labels arange + off
+hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, int off, hipStream_t s);
 hipError_t launch_sparc_local(float* part, const float* S, const float* mask, int B, int T, hipStream_t s);
-hipError_t launch_sparc_loss_finish(float* out, const float* lr, const float* lc, const float* part, int B,
-                                    float global_weight, float local_weight, hipStream_t s);
+// parts[5] = {sum lr, sum lc, sum part[.][0], sum part[.][1], sum part[.][2]} of one shard
+hipError_t launch_loss_parts(float* parts, const float* lr, const float* lc, int R, const float* part, int B,
+                             hipStream_t s);
+// out = wg (P0 + P1) / (2 N) + wl (P2 + P3) / (2 P4)   (wl == 0: no local term)
+hipError_t launch_loss_combine(float* out, const float* parts, int N, float global_weight, float local_weight,
+                               hipStream_t s);
 
 // Device image preprocessing (preprocess.hip).  Per image: source offset/size, the source rows
 // the vertical taps touch [ybase, ybase + nrows), the intermediate's offset, and tap tables:

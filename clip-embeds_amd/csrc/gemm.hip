@@ -2843,6 +2843,8 @@ int set_gemm_schedule(int v) {
     return prev;
 }
 
+int current_gemm_sched() { return gemm_sched(); }
+
 void set_gemm_trace(unsigned long long* buf, long n) {
     g_trace = buf;
     g_trace_n = buf ? n : 0;
@@ -2856,8 +2858,9 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.m_dev) {
-        // packed rows: the folded-tower epilogues on one tile per workgroup, no split-K
-        if ((epi != EPI_LN_FOLD && epi != EPI_LN_STATS_HL) || gemm_sched() == 12) return hipErrorInvalidValue;
+        // packed rows: the folded-tower epilogues on one tile per workgroup, no split-K; only the default
+        // schedule's kernels clip at the device row count (run_text turns the packing off otherwise)
+        if ((epi != EPI_LN_FOLD && epi != EPI_LN_STATS_HL) || gemm_sched() != 1) return hipErrorInvalidValue;
         p.onetile = 1;
         p.part = nullptr;
         p.part_elems = 0;

@@ -613,8 +613,9 @@ __global__ __launch_bounds__(256) void mean_mid_k(const float* __restrict__ x, f
     out[(size_t)b * D + d] = acc / (float)P;
 }
 
-// loss[i] = logsumexp_j L[i][j] - L[i][i]  (F.cross_entropy against arange labels, per row); wave per row
-__global__ __launch_bounds__(256) void ce_diag_rows_k(const float* __restrict__ L, int R, int C,
+// loss[i] = logsumexp_j L[i][j] - L[i][off + i]  (F.cross_entropy against labels arange + off, per row;
+// off = the first global row of this rank's shard, loss.py:113-117 local-loss labels); wave per row
+__global__ __launch_bounds__(256) void ce_diag_rows_k(const float* __restrict__ L, int R, int C, int off,
                                                       float* __restrict__ loss) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(256) void ce_diag_rows_k(const float* __restrict__ 
     float sum = 0.f;
     for (int j = lane; j < C; j += 64) sum += __expf(lr[j] - m);
     sum = wave_sum(sum);
-    if (lane == 0) loss[row] = logf(sum) + m - lr[row];
+    if (lane == 0) loss[row] = logf(sum) + m - lr[off + row];
 }
 
 // Masked pairwise local loss, both directions, for one sample per block (pacl.py:527-562):
@@ -670,15 +671,19 @@ __global__ __launch_bounds__(256) void sparc_local_k(const float* __restrict__ S
     }
 }
 
-// total = wg * (mean(lr) + mean(lc)) / 2 + wl * (P0 / M + P1 / M) / 2; fixed summation order
-__global__ __launch_bounds__(256) void sparc_loss_finish_k(const float* __restrict__ lr, const float* __restrict__ lc,
-                                                           const float* __restrict__ part, int B, float wg, float wl,
-                                                           float* __restrict__ out) {
+// Partial sums of one shard, fixed summation order: parts = {sum_i lr_i, sum_i lc_i, sum_b part[b][0],
+// sum_b part[b][1], sum_b part[b][2]} (lr / lc / part may be null: those sums are 0).  The shards' parts
+// add up (caller's all-reduce) to the sums over the whole batch.
+__global__ __launch_bounds__(256) void loss_parts_k(const float* __restrict__ lr, const float* __restrict__ lc,
+                                                    int R, const float* __restrict__ part, int B,
+                                                    float* __restrict__ parts) {
     float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i = threadIdx.x; i < B; i += 256) {
-        v[0] += lr[i]; v[1] += lc[i];
-        v[2] += part[3 * i]; v[3] += part[3 * i + 1]; v[4] += part[3 * i + 2];
-    }
+    if (lr)
+        for (int i = threadIdx.x; i < R; i += 256) { v[0] += lr[i]; v[1] += lc[i]; }
+    if (part)
+        for (int i = threadIdx.x; i < B; i += 256) {
+            v[2] += part[3 * i]; v[3] += part[3 * i + 1]; v[4] += part[3 * i + 2];
+        }
     __shared__ float red[5][4];
     const int wv = threadIdx.x >> 6;
 #pragma unroll
@@ -687,13 +692,20 @@ __global__ __launch_bounds__(256) void sparc_loss_finish_k(const float* __restri
         if ((threadIdx.x & 63) == 0) red[k][wv] = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float t[5];
-        for (int k = 0; k < 5; ++k) t[k] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
-        const float glob = (t[0] / (float)B + t[1] / (float)B) * 0.5f;
-        const float local = (t[2] / t[4] + t[3] / t[4]) * 0.5f;
-        out[0] = wg * glob + wl * local;
+    if (threadIdx.x < 5) {
+        const int k = threadIdx.x;
+        parts[k] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
     }
+}
+
+// total = wg * (P0 / N + P1 / N) / 2 + wl * (P2 / P4 + P3 / P4) / 2   (pacl.py:567-583; wl == 0: the
+// PACL ClipLoss, pacl.py:509-512, no local term)
+__global__ void loss_combine_k(const float* __restrict__ parts, int N, float wg, float wl, float* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    const float glob = (parts[0] / (float)N + parts[1] / (float)N) * 0.5f;
+    float total = wg * glob;
+    if (wl != 0.f) total += wl * ((parts[2] / parts[4] + parts[3] / parts[4]) * 0.5f);
+    out[0] = total;
 }
 
 }  // namespace
@@ -702,18 +714,23 @@ hipError_t launch_mean_mid(float* out, const float* x, int B, int P, int D, hipS
     hipLaunchKernelGGL(mean_mid_k, dim3((unsigned)((D + 255) / 256), (unsigned)B), dim3(256), 0, s, x, out, P, D);
     return hipGetLastError();
 }
-hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, hipStream_t s) {
-    hipLaunchKernelGGL(ce_diag_rows_k, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, L, R, C, loss);
+hipError_t launch_ce_diag_rows(float* loss, const float* L, int R, int C, int off, hipStream_t s) {
+    if (R <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ce_diag_rows_k, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, s, L, R, C, off, loss);
     return hipGetLastError();
 }
 hipError_t launch_sparc_local(float* part, const float* S, const float* mask, int B, int T, hipStream_t s) {
     hipLaunchKernelGGL(sparc_local_k, dim3((unsigned)B), dim3(128), 0, s, S, mask, T, part);
     return hipGetLastError();
 }
-hipError_t launch_sparc_loss_finish(float* out, const float* lr, const float* lc, const float* part, int B,
-                                    float global_weight, float local_weight, hipStream_t s) {
-    hipLaunchKernelGGL(sparc_loss_finish_k, dim3(1), dim3(256), 0, s, lr, lc, part, B, global_weight, local_weight,
-                       out);
+hipError_t launch_loss_parts(float* parts, const float* lr, const float* lc, int R, const float* part, int B,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(loss_parts_k, dim3(1), dim3(256), 0, s, lr, lc, R, part, B, parts);
+    return hipGetLastError();
+}
+hipError_t launch_loss_combine(float* out, const float* parts, int N, float global_weight, float local_weight,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(loss_combine_k, dim3(1), dim3(64), 0, s, parts, N, global_weight, local_weight, out);
     return hipGetLastError();
 }
 

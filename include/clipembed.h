@@ -230,6 +230,34 @@ int ce_sparc_loss(ce_handle* h, void* stream, const float* v_patch, const float*
                   const float* mask, int B, int P, int T, int D, float temperature, float global_weight,
                   float local_weight, float* out_loss);
 
+/* The same losses over a global batch sharded across data-parallel ranks.  train_sparc.py:93,105 and
+ * train_pacl.py:34-36,95,106 wrap the model in nn.DataParallel: every replica's outputs are gathered to
+ * one device and SparcLoss / ClipLoss(0.1) run on the WHOLE batch there.  Here each rank keeps its B
+ * samples and the loss value is the reference's global one, in three steps around two collectives the
+ * caller issues (RCCL all-gather of the [B,D] features in rank order, RCCL all-reduce (sum) of 5 floats):
+ *   ce_sparc_loss_means          out_img / out_txt [B,D] = L2norm(mean_p v_patch), L2norm(mean_t l_tokens)
+ *                                (pacl.py:561-562) — the features the ranks all-gather into img_all /
+ *                                txt_all [Bg,D];
+ *   ce_sparc_loss_partial        parts[5] (device f32, overwritten) = this shard's sums over its rows
+ *                                r = row0..row0+B-1 of the global CE both ways (logits 1/temperature *
+ *                                img_all[r] . txt_all^T, label r; pacl.py:563-570), then the masked local
+ *                                CE sums both ways and the mask count (pacl.py:522-556,575-580) over its
+ *                                samples (l_tokens, grouped, mask as for ce_sparc_loss);
+ *   ce_contrastive_loss_partial  parts[0..1] as above for the PACL ClipLoss (pacl.py:498-512; features
+ *                                already normalised, logit scale `scale`), parts[2..4] = 0;
+ *   ce_loss_combine              out_loss = global_weight (P0 + P1) / (2 n_global) + local_weight (P2 + P3)
+ *                                / (2 P4) over the all-reduced parts (local_weight 0: no local term).
+ * One rank (row0 = 0, B = Bg) gives ce_sparc_loss's value; the shards' sums add up to it in any split. */
+int ce_sparc_loss_means(ce_handle* h, void* stream, const float* v_patch, const float* l_tokens, int B, int P, int T,
+                        int D, float* out_img, float* out_txt);
+int ce_sparc_loss_partial(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg, int row0,
+                          const float* l_tokens, const float* grouped, const float* mask, int B, int T, int D,
+                          float temperature, float* parts);
+int ce_contrastive_loss_partial(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg,
+                                int row0, int B, int D, float scale, float* parts);
+int ce_loss_combine(ce_handle* h, void* stream, const float* parts, int n_global, float global_weight,
+                    float local_weight, float* out_loss);
+
 /* apply_rope (pacl.py:147-181): de-interleaving rotary embedding over positions 0..P-1.
  * x, out: device f32 [B,P,D] (may alias). */
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out);
@@ -285,7 +313,8 @@ int ce_set_gemm_variant(int bits);
  * sums taken by the MFMA), 4 = one barrier per key tile, 8 = 16-B output stores, 16 = V^T fragments
  * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
  * offset too (row sums checked from both sides), 64 = K/V DMAs through row-clipped buffer descriptors.
- * Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125; anything
+ * 128 = three K/V LDS slots (the next-but-one tile's DMA in flight; A/B only, measured slower: 3 workgroups
+ * per CU instead of 4).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 253; anything
  * else restores the default (125).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);

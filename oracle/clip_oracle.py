@@ -263,3 +263,53 @@ def negclip_local_loss(imgs, txts, per_rank_B, rank, scale):
     li = np.arange(per_rank_B) + per_rank_B * rank
     lt = np.concatenate([li, -100 * np.ones(txts[rank].shape[0] - per_rank_B, dtype=np.int64)])
     return (cross_entropy(lpi, li) + cross_entropy(lpt, lt)) / 2
+
+
+# ------------------------------------------------------------------ sharded losses (test doubles)
+def _ce_row_sums(logits, row0):
+    """sum over rows i of (logsumexp_j logits[i] - logits[i, row0 + i])  (pacl.py:509-512 summed)."""
+    m = logits.max(-1, keepdims=True)
+    lse = np.log(np.exp((logits - m).astype(np.float64)).sum(-1)) + m[:, 0]
+    return float((lse - logits[np.arange(logits.shape[0]), row0 + np.arange(logits.shape[0])]).sum())
+
+
+def contrastive_loss_parts(img_all, txt_all, row0, B, scale):
+    """ce_contrastive_loss_partial: this shard's CE sums of its rows of the global logits both ways
+    (ClipLoss.forward, pacl.py:498-512, on the gathered batch)."""
+    s = F32(scale)
+    return np.array([_ce_row_sums(s * img_all[row0:row0 + B] @ txt_all.T, row0),
+                     _ce_row_sums(s * txt_all[row0:row0 + B] @ img_all.T, row0), 0.0, 0.0, 0.0], np.float64)
+
+
+def sparc_loss_means(v_patch, l_tokens):
+    """ce_sparc_loss_means: the normalised patch / token means (pacl.py:561-562)."""
+    return l2normalize(v_patch.mean(1)), l2normalize(l_tokens.mean(1))
+
+
+def _masked_pairwise_sums(a, b, mask, scale):
+    """(sum of masked CE, mask sum) of masked_pairwise_contrastive_loss (pacl.py:522-556)."""
+    logits = (np.einsum("bmd,bnd->bmn", a, b) * F32(scale)).astype(F32)
+    logits = logits + ((F32(1.0) - mask) * F32(-1e8))[:, None, :]
+    m = logits.max(-1, keepdims=True)
+    lse = np.log(np.exp((logits - m).astype(np.float64)).sum(-1)) + m[..., 0]
+    T = a.shape[1]
+    loss = lse - logits[:, np.arange(T), np.arange(T)]
+    return float((loss * mask).sum()), float(mask.sum())
+
+
+def sparc_loss_parts(img_all, txt_all, row0, l_tokens, grouped, mask, temperature=0.1):
+    """ce_sparc_loss_partial: global CE sums of the shard's rows + masked local sums of its samples."""
+    s = 1.0 / temperature
+    p = contrastive_loss_parts(img_all, txt_all, row0, l_tokens.shape[0], s)
+    p[2], cnt = _masked_pairwise_sums(grouped, l_tokens, mask, s)
+    p[3], _ = _masked_pairwise_sums(l_tokens, grouped, mask, s)
+    p[4] = cnt
+    return p
+
+
+def loss_combine(parts, n_global, global_weight, local_weight):
+    """ce_loss_combine: wg (P0 + P1) / (2 N) + wl (P2 + P3) / (2 P4)  (pacl.py:567-583)."""
+    out = global_weight * (parts[0] / n_global + parts[1] / n_global) / 2
+    if local_weight != 0:
+        out += local_weight * (parts[2] / parts[4] + parts[3] / parts[4]) / 2
+    return float(out)

@@ -7,7 +7,14 @@ towers is depth-independent) and the deterministic synthetic weights / PACL-shap
 without the network fetch in the constructor (the same head modules, pacl.py:397-406).  Writes
 outputs only: selected token / patch rows of forward(), both scoring() modes and SparcLoss.
 
-    python tests/golden/make_golden_sparc.py   ->  tests/golden/sparc_full.npz
+    python tests/golden/make_golden_sparc.py        ->  tests/golden/sparc_full.npz
+    python tests/golden/make_golden_sparc.py dist   ->  tests/golden/sparc_dist.npz
+
+`dist`: the reference SparcLoss(0.1) (train_sparc.py:105) and PACL ClipLoss(0.1) (train_pacl.py:106)
+on the CONCATENATION of two ranks' shards (tests/golden/dist_inputs.py), i.e. the value
+train_sparc.py / train_pacl.py compute after nn.DataParallel gathers the replicas' outputs to one
+device (train_sparc.py:93, train_pacl.py:95); plus each shard's own single-process loss, which the
+sharded path must NOT return.
 """
 import os
 import sys
@@ -77,5 +84,29 @@ def main():
     print("wrote", path, {k: v.shape for k, v in out.items()})
 
 
+def main_dist():
+    import torch
+    from dist_inputs import pacl_shard, sparc_shard
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    _, _, pacl_mod = MG.import_reference()
+    sh = [sparc_shard(r) for r in range(2)]
+    ph = [pacl_shard(r) for r in range(2)]
+    cat = lambda k, xs: torch.from_numpy(np.concatenate([x[k] for x in xs]))   # noqa: E731
+    out = {}
+    with torch.no_grad():
+        sl = pacl_mod.SparcLoss(0.1)
+        out["sparc_global"] = np.float32(sl(cat(0, sh), cat(1, sh), cat(2, sh), cat(3, sh)).item())
+        cl = pacl_mod.ClipLoss(0.1)
+        out["pacl_global"] = np.float32(cl(cat(0, ph), cat(1, ph)).item())
+        for r in range(2):
+            t = [torch.from_numpy(x) for x in sh[r]]
+            out[f"sparc_shard_r{r}"] = np.float32(sl(*t).item())
+            out[f"pacl_shard_r{r}"] = np.float32(cl(*[torch.from_numpy(x) for x in ph[r]]).item())
+    path = os.path.join(HERE, "sparc_dist.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, out)
+
+
 if __name__ == "__main__":
-    main()
+    main_dist() if sys.argv[1:] == ["dist"] else main()

@@ -141,3 +141,86 @@ def test_train_feature_grad_two_ranks(golden):
         # d loss / d logit_scale = scale * d loss / d scale (the reference differentiates w.r.t. scale)
         np.testing.assert_allclose(got[r]["dlogit_scale"], 12.5 * float(g[f"dscale_r{r}"]), rtol=1e-4)
         np.testing.assert_allclose(got[r]["dtxt"], g[f"dtxt_r{r}"], rtol=1e-4, atol=1e-7)
+
+
+def _loss_worker(rank, world, port, q):
+    """clipembed.pacl.SparcLoss / ClipLoss(rank, world_size) on 2 gloo ranks: the product's exchange
+    (all-gather of the [B,768] means / features, shard row offsets, all-reduce of the 5 partial sums)
+    with the oracle's arithmetic in place of the engine calls (test double: no device here)."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "clip-embeds_amd"), repo, os.path.join(repo, "tests", "golden")]
+    from clipembed.pacl import ClipLoss, SparcLoss
+    from dist_inputs import pacl_shard, sparc_shard
+    from oracle import clip_oracle as O
+
+    class Double:
+        def _engine(self, t):
+            return None
+
+        def _contrastive_parts(self, e, img_all, txt_all, row0, B):
+            return torch.from_numpy(O.contrastive_loss_parts(img_all.numpy(), txt_all.numpy(), row0, B,
+                                                             self.logit_scale).astype(np.float32))
+
+        def _combine(self, e, parts, n, wg, wl):
+            return torch.tensor(O.loss_combine(parts.double().numpy(), n, wg, wl))
+
+        def _means(self, e, v, lt):
+            gi, gt = O.sparc_loss_means(v.numpy(), lt.numpy())
+            return torch.from_numpy(gi), torch.from_numpy(gt)
+
+        def _sparc_parts(self, e, img_all, txt_all, row0, lt, g, m):
+            return torch.from_numpy(O.sparc_loss_parts(img_all.numpy(), txt_all.numpy(), row0, lt.numpy(), g.numpy(),
+                                                       m.numpy(), 1.0 / self.logit_scale).astype(np.float32))
+
+    class CpuSparcLoss(Double, SparcLoss):
+        pass
+
+    class CpuClipLoss(Double, ClipLoss):
+        pass
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v, l, g, m = (torch.from_numpy(x) for x in sparc_shard(rank))
+    img, txt = (torch.from_numpy(x) for x in pacl_shard(rank))
+    res = {"sparc": float(CpuSparcLoss(0.1, rank=rank, world_size=world)(v, l, g, m)),
+           "pacl": float(CpuClipLoss(0.1, rank=rank, world_size=world)(img, txt))}
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sparc_pacl_global_loss_two_ranks(golden):
+    """Every rank returns the reference's loss over the WHOLE 2-rank batch (train_sparc.py:93,105 /
+    train_pacl.py:34-36,95: DataParallel gathers, the loss runs on the global batch), not its shard's."""
+    g = golden("sparc_dist")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loss_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        np.testing.assert_allclose(got[r]["sparc"], float(g["sparc_global"]), rtol=1e-5, err_msg=f"rank {r}")
+        np.testing.assert_allclose(got[r]["pacl"], float(g["pacl_global"]), rtol=1e-5, err_msg=f"rank {r}")
+        assert abs(got[r]["sparc"] - float(g[f"sparc_shard_r{r}"])) > 0.05     # not the shard-local value
+        assert abs(got[r]["pacl"] - float(g[f"pacl_shard_r{r}"])) > 0.05
+
+
+def test_oracle_shard_parts_add_up(golden):
+    """The oracle's shard decomposition (the arithmetic ce_sparc_loss_partial / ce_loss_combine
+    follow) reproduces the reference's one-shard losses too."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from dist_inputs import sparc_shard
+    from oracle import clip_oracle as O
+    g = golden("sparc_dist")
+    for r in range(2):
+        v, l, gr, m = sparc_shard(r)
+        gi, gt = O.sparc_loss_means(v, l)
+        p = O.sparc_loss_parts(gi, gt, 0, l, gr, m, 0.1)
+        np.testing.assert_allclose(O.loss_combine(p, 4, 0.5, 1.0), float(g[f"sparc_shard_r{r}"]), rtol=1e-5)

@@ -369,6 +369,29 @@ def test_attention_wide_scores(scale, attn_var):
     assert err0 < 2e-2 * max(1.0, ref.abs().max().item()), err0
 
 
+def attn_ref_f32(qkv, B, L, H, causal):
+    """softmax(q k^T / 8) v in plain f32 on the bf16 inputs, no kernel rounding restated."""
+    x = qkv.float().reshape(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (x[0] @ x[1].transpose(-1, -2)) / 8.0
+    if causal:
+        s = s + torch.triu(torch.full((L, L), float("-inf"), device=qkv.device), 1)
+    return (s.softmax(-1) @ x[2]).permute(0, 2, 1, 3).reshape(B * L, H * 64)
+
+
+@pytest.mark.parametrize("scale,causal", [(3.0, False), (4.5, False), (3.0, True)])
+def test_attention_wide_scores_vs_unrounded_f32(scale, causal):
+    """The default kernel against attention in f32 WITHOUT the kernel's bf16(q * log2(e)/8) input
+    rounding (attn_ref restates it): bounds that rounding's effect at kernel level, on score spreads
+    of tens of log2 units (the bound of the rounding-free reference before it was restated)."""
+    B, L, H = 2, (577 if not causal else 77), 4
+    g = torch.Generator(device="cpu").manual_seed(int(scale * 10) + causal)
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    out = run_attn(qkv, B, L, H, causal)
+    ref = attn_ref_f32(qkv, B, L, H, causal)
+    err = (out.float() - ref).abs().max().item()
+    assert err < 6e-2 * max(1.0, ref.abs().max().item()), err
+
+
 @pytest.mark.parametrize("rows,D,bf16", [(1000, 1024, True), (1000, 1024, False), (77, 768, True), (3, 768, False)])
 def test_layernorm(rows, D, bf16):
     g = torch.Generator(device="cpu").manual_seed(rows + D)

@@ -7,6 +7,7 @@
 #   rocprof:<bench.py args>                rocprofv3 --kernel-trace --stats of one bench.py run
 #   clock:<bench.py args>                  GRBM_GUI_ACTIVE pass (effective clock per kernel)
 #   pmc:<counter>,<bench.py args>          one --pmc pass with one counter over a short bench run
+#   pmcs:<c1+c2+...>,<bench.py args>       one --pmc pass with several counters (within one pass's limits)
 #   py:<script>,<args>                     any python script (kernel A/B: tools/bench_gemm_epi.py,
 #                                          tools/bench_kernels.py; timelines: tools/gemm_trace.py)
 # Every step has its own time limit; the chain stops at the first failure.
@@ -34,6 +35,10 @@ for step in "$@"; do
              timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $cnt -d gpurun_out/${TAG}_pmc${n}_$cnt \
                -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-timing $rest \
                > gpurun_out/${TAG}_pmc${n}.log 2>&1 ;;
+    pmcs)    cnt=${args%% *}; rest=${args#* }; [ "$rest" = "$args" ] && rest=""; cnt=${cnt//+/ }
+             timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $cnt -d gpurun_out/${TAG}_pmcs$n \
+               -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-timing $rest \
+               > gpurun_out/${TAG}_pmcs${n}.log 2>&1 ;;
     py)      timeout -k 10 600 python -u $args > gpurun_out/${TAG}_py$n.log 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
