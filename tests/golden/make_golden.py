@@ -261,5 +261,24 @@ def main():
     save(out)
 
 
+def main_pacl_full():
+    """pacl_full.npz: the three open_clip_pacl variants + the sigmoid(10 cos) weighting around the
+    FULL-depth (24 + 12 blocks) reference CLIP ViT-L/14-336, diag pairing of 2 images x 2 captions
+    and the 1 image x 2 captions broadcast (Q6); plus the token / patch-head rows."""
+    import torch
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    model_mod, _, pacl_mod = import_reference()
+    base = get_model_config("ViT-L-14-336")
+    clip_model, _ = build_clip(model_mod, base)
+    out = {}
+    gen_pacl(pacl_mod, clip_model, base, out)
+    res = out["pacl"]
+    res["images_seed"] = np.int64(1100)
+    res["captions_seed"] = np.int64(2100)
+    save({"pacl_full": res})
+
+
 if __name__ == "__main__":
-    main()
+    main_pacl_full() if sys.argv[1:] == ["pacl_full"] else main()

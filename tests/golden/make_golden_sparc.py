@@ -8,6 +8,7 @@ without the network fetch in the constructor (the same head modules, pacl.py:397
 outputs only: selected token / patch rows of forward(), both scoring() modes and SparcLoss.
 
     python tests/golden/make_golden_sparc.py        ->  tests/golden/sparc_full.npz
+    python tests/golden/make_golden_sparc.py fulldepth   ->  tests/golden/sparc_fulldepth.npz (24 + 12 blocks)
     python tests/golden/make_golden_sparc.py dist   ->  tests/golden/sparc_dist.npz
 
 `dist`: the reference SparcLoss(0.1) (train_sparc.py:105) and PACL ClipLoss(0.1) (train_pacl.py:106)
@@ -50,14 +51,16 @@ def build_sparc(pacl_mod, clip_model, cls, heads_sd, sigma):
     return obj
 
 
-def main():
+def main(full_depth=False):
     import torch
     from clipembed import weights as W
     from clipembed.config import get_model_config
     torch.set_num_threads(8)
     torch.use_deterministic_algorithms(True)
     model_mod, _, pacl_mod = MG.import_reference()
-    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    cfg = get_model_config("ViT-L-14-336")
+    if not full_depth:
+        cfg = cfg.with_depth(1, 1)
     clip, _ = MG.build_clip(model_mod, cfg)
     heads = W.synthetic_pacl_heads(cfg.with_pacl(768))
     imgs = torch.from_numpy(W.synthetic_images(2, seed=1300))
@@ -79,7 +82,7 @@ def main():
             out[f"{tag}_score_global"] = mod.scoring(imgs, caps, local=False).numpy()
             out[f"{tag}_score_bcast"] = mod.scoring(imgs[:1], caps, local=True).numpy()   # 1 image x 2 captions
             out[f"{tag}_loss"] = np.float32(pacl_mod.SparcLoss(0.07)(v, l, g, mask).item())
-    path = os.path.join(HERE, "sparc_full.npz")
+    path = os.path.join(HERE, "sparc_fulldepth.npz" if full_depth else "sparc_full.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, {k: v.shape for k, v in out.items()})
 
@@ -109,4 +112,7 @@ def main_dist():
 
 
 if __name__ == "__main__":
-    main_dist() if sys.argv[1:] == ["dist"] else main()
+    if sys.argv[1:] == ["dist"]:
+        main_dist()
+    else:
+        main(full_depth=sys.argv[1:] == ["fulldepth"])
