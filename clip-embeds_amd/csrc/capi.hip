@@ -155,6 +155,11 @@ struct ce_handle {
     bool timing = false;
     std::string timing_only;     // non-empty: only launches with this tag are bracketed
     float* cur_part = nullptr;   // GEMM split-K slabs of the tower whose launches are being issued
+    // packed text rows (pooled-only calls): the sequence offsets of the last launch, read back on the
+    // host during a full profile pass only (every launch timed, no filter), so that the per-kernel
+    // table carries the packed launches' work; seg_dev identifies the device copy they describe
+    std::vector<int> seg_host;
+    const int* seg_dev = nullptr;
     // LayerNorm folding of the vision blocks: enabled unless CE_LN_FOLD=0 /
     // ce_set_ln_fold(h, 0); folded[name] = "<name>@fold{,_c,_d}" are current for weight `name`
     bool ln_fold = true;
@@ -470,8 +475,13 @@ int gemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda
     const double bytes = 2.0 * ((double)M * K + (double)N * K) + (double)M * N * (out_bf16 ? 2 : 4) +
                          ((resid || hl) ? (double)M * N * 4 : 0.0) +
                          (ea.xb && ea.epi == ce::EPI_LN_STATS ? (double)M * N * 2 : 0.0);
-    // (packed rows: the live count is known on the device only; the work is not reported)
-    return timed(h, s, tag, ea.m_dev ? 0.0 : flops, ea.m_dev ? 0.0 : bytes,
+    // packed rows: the live count is on the device; a full profile pass has read it back (seg_host)
+    double work = 1.0;
+    if (ea.m_dev) {
+        const bool known = h->seg_dev && ea.m_dev == h->seg_dev + (h->seg_host.size() - 1);
+        work = known && M > 0 ? (double)h->seg_host.back() / M : 0.0;
+    }
+    return timed(h, s, tag, flops * work, bytes * work,
                  [&] { return ce::launch_gemm(p, act, out_bf16, s, ea.epi); });
 }
 
@@ -588,8 +598,19 @@ int run_block_folded(ce_handle* h, hipStream_t s, const TowerWs& w, const Blk& k
     CE_TRY(gemm(h, s, vis ? "gemm_qkv_v" : "gemm_qkv_t", w.xn, D, f.wqkv, M, 3 * D, D, f.dqkv, ce::ACT_NONE_,
                 nullptr, w.qkv, true, 0, 0, 0, 0, 0, fold));
     {
-        const double flops = seg ? 0.0 : 4.0 * B * H * (double)L * L * 64;
-        const double bytes = seg ? 0.0 : (double)M * 3 * D * 2 + (double)M * D * 2;
+        double flops = 4.0 * B * H * (double)L * L * 64;
+        double bytes = (double)M * 3 * D * 2 + (double)M * D * 2;
+        if (seg) {
+            // packed causal sequences of n_b = EOT + 1 rows: the full n_b x n_b score matrix each (as the
+            // reference's count of a forward), when a profile pass has read the offsets back
+            flops = bytes = 0.0;
+            if (seg == h->seg_dev && (int)h->seg_host.size() == B + 1)
+                for (int b = 0; b < B; ++b) {
+                    const double n = h->seg_host[b + 1] - h->seg_host[b];
+                    flops += 4.0 * H * n * n * 64;
+                    bytes += n * (3 * D * 2 + D * 2);
+                }
+        }
         CE_TRY(timed(h, s, vis ? "attn_v" : "attn_t", flops, bytes,
                      [&] { return ce::launch_attention(w.qkv, w.att, B, L, H, !vis, true, s, nullptr, seg); }));
     }
@@ -756,6 +777,16 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
                        ce::current_gemm_sched() == 1;
     const int* seg = prune ? w.seg : nullptr;
     if (prune) CE_TRY(check_launch(ce::launch_text_pack(w.rows, w.seg, ids, B, L, s), "text_pack"));
+    h->seg_dev = nullptr;
+    h->seg_host.clear();
+    if (prune && h->timing && h->timing_only.empty()) {
+        // full profile pass (every launch bracketed, outside any timed region): read the packed
+        // sequence offsets back once so the packed launches report their work
+        h->seg_host.resize(B + 1);
+        HIP_TRY(hipMemcpyAsync(h->seg_host.data(), w.seg, (B + 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        h->seg_dev = w.seg;
+    }
     else if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     if (use_fold) {
         CE_TRY(timed(h, s, "t_embed", 0.0, (double)B * L * D * (h->resid_hl ? 12.0 : 10.0), [&] {
