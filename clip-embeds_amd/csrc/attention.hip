@@ -83,6 +83,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     constexpr bool ASMV = (VAR & 16) != 0;   // V^T reads by inline asm (no vmcnt(0) before P.V)
     constexpr bool FAST0 = (VAR & 32) != 0;  // tile 0 on the fixed offset too (two-sided check)
     constexpr bool BUFDMA = (VAR & 64) != 0; // K/V DMAs through clipped buffer descriptors
+    // CLSK (bit 256, non-causal, (L - 1) % 64 == 0): key 0 (the CLS token) enters the softmax up
+    // front (one 64-d dot product per query on the VALU, O and l initialised with its term) and the
+    // key tiles cover keys 1..L-1: L = 577 runs 9 full tiles instead of 9 + one single-key tile on the
+    // masked general path
+    constexpr bool CLSK = !CAUSAL && (VAR & 256) != 0;
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -136,17 +141,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int spos = tid & 7;
     const int kchunk = spos ^ ((tid >> 4) & 7);
     const int vchunk = spos ^ (((srow >> 1) & 1) << 2);   // V image swizzle (conflict-free tr reads)
-    const int kv_end = CAUSAL ? min(L, qb * QBLK + QBLK) : L;
+    const int Lk = CLSK ? L - 1 : L;                     // keys covered by the tiles
+    const int kv_end = CAUSAL ? min(L, qb * QBLK + QBLK) : Lk;
     const int nkt = (kv_end + KBLK - 1) / KBLK;
-    const bf16_t* kbase = base + D + h * 64;
-    const bf16_t* vbase = base + 2 * D + h * 64;
+    const bf16_t* kbase = base + D + h * 64 + (CLSK ? ld : 0);
+    const bf16_t* vbase = base + 2 * D + h * 64 + (CLSK ? ld : 0);
 
     // BUFDMA: the K / V columns of this (b, h) as buffer descriptors clipped after row L - 1 (rows
     // past the end read zeros: masked keys), per-lane row/chunk offsets computed once, the tile's
     // row offset one scalar add per DMA (the flat form rebuilt 64-bit addresses with 64-bit
     // multiplies for every DMA)
     const int ld2 = (int)ld * 2;
-    const int nrec = BUFDMA ? (L - 1) * ld2 + 128 : 0;
+    const int nrec = BUFDMA ? (Lk - 1) * ld2 + 128 : 0;
     const __amdgpu_buffer_rsrc_t ksrd = attn_srd(kbase, nrec);
     const __amdgpu_buffer_rsrc_t vsrd = attn_srd(vbase, nrec);
     int kvo[2] = {0, 0}, vvo[2] = {0, 0};
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         }
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
-            const int key = min(t * KBLK + ps * 32 + srow, L - 1);
+            const int key = min(t * KBLK + ps * 32 + srow, Lk - 1);
             glds16(kbase + (size_t)key * ld + kchunk * 8, dst + ps * 4096);
             glds16(vbase + (size_t)key * ld + vchunk * 8, dst + TILE_KV_BYTES + ps * 4096);
         }
@@ -216,6 +222,37 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     // to l = 0 later); a row outside sends tile 0 to the general path, which sets the exact max
     bool fast = MODE >= 1 && FAST0;
     const f32x16 zero16 = {};
+    // CLSK: key 0's score (log2 units, both lane halves) and its term in O / l.  Offset 0 (the fixed
+    // offset) when every query of the wave has |s0| <= 64, else the exact s0 (general path)
+    float s0v = 0.f;
+    bool fix_ok = true;                      // wave-uniform: the offset may stay fixed at 0
+    if constexpr (CLSK) {
+        const bf16_t* k0 = base + D + h * 64 + 8 * h2;
+        float a = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf((float)qf[ks][e], (float)kv[e], a);
+        }
+        s0v = a + __shfl_xor(a, 32, 64);
+        fix_ok = MODE >= 1 && __all(s0v <= 64.0f && s0v >= -64.0f);
+        float p0 = 1.0f;
+        if (fix_ok) p0 = __builtin_amdgcn_exp2f(s0v);
+        else { m_run = s0v; fast = false; }
+        if (h2 == 0) l_run = p0;
+        const bf16_t* v0 = base + 2 * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
+                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
+                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
+                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
+                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
+            }
+    }
 
     // O^T += V^T P^T with the V^T fragments read by inline asm (no wait on the LDS-DMA in flight):
     // the reads of 16-key group q + 1 are issued before the MFMAs of group q, counted lgkmcnt.
@@ -329,10 +366,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         const bool active = q_wave0 < L && !(CAUSAL && t * KBLK > q_wave0 + 31);
         // second 32-key subtile entirely past the sequence end (L = 577: the last tile holds one
         // key) or (causal) entirely above this wave's diagonal: skip its MFMAs and exponentials
-        const bool half2 = (t * KBLK + 32 < L) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
+        const bool half2 = (t * KBLK + 32 < Lk) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
         const int key0 = t * KBLK;
         // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
-        const bool need_mask = (key0 + KBLK > L) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
+        const bool need_mask = (key0 + KBLK > Lk) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
         const bool fast_tile = MODE >= 1 && fast && half2 && !need_mask;   // wave-uniform
         bool redo = false;
         if (active && fast_tile) {
@@ -422,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
-                        const bool masked = (key >= L) || (CAUSAL && key > qrow);
+                        const bool masked = (key >= Lk) || (CAUSAL && key > qrow);
                         s[kt2][i] = masked ? -INFINITY : s[kt2][i];
                     }
             }
@@ -438,11 +475,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             // from the f32 / bf16 overflow and O / l are rarely rescaled.  O and l always see the
             // same factor, and the decision precedes this tile's P, so no P.V product straddles it.
             // VARs >= 1: when tile 0's row maxima all lie within +-64, the offset stays 0.
-            const bool fix0 = MODE >= 1 && t == 0 && __all(tmax <= 64.0f && tmax >= -64.0f);
+            // (CLSK: O / l already hold key 0's term, so the first move rescales them, and the exact
+            // max includes key 0; the fixed offset needs key 0 on it too)
+            const bool fix0 = MODE >= 1 && t == 0 && fix_ok && __all(tmax <= 64.0f && tmax >= -64.0f);
             if (fix0) fast = true;
             if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
-                const float delta = t == 0 ? tmax : fmaxf(tmax, 0.f);
-                if (t != 0) rescale(delta);
+                const float delta = t == 0 ? (CLSK ? fmaxf(tmax, s0v - m_run) : tmax) : fmaxf(tmax, 0.f);
+                if (t != 0 || CLSK) rescale(delta);
                 else m_run += delta;
                 fast = false;
     #pragma unroll
@@ -680,7 +719,10 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else if (v & 8) CE_ATTN_LAUNCH(true, 8);
         else CE_ATTN_LAUNCH(true, 0);
     } else {
-        switch (v) {
+        // CLSK needs the keys after the first to fill whole tiles
+        const int vv = (v & 256) && !((L - 1) % KBLK == 0 && L > 1) ? (v & ~256) : v;
+        switch (vv) {
+            case 381: CE_ATTN_LAUNCH(false, 381); break;
             case 125: CE_ATTN_LAUNCH(false, 125); break;
             case 253: CE_ATTN_LAUNCH(false, 253); break;
             case 61: CE_ATTN_LAUNCH(false, 61); break;
@@ -702,7 +744,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 int set_attn_variant(int var) {
     const int prev = g_attn_var;
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61 || var == 125 || var == 253)
+                  var == 61 || var == 125 || var == 253 || var == 381)
                      ? var : 125;
     return prev;
 }

@@ -287,7 +287,7 @@ def attn_ref(qkv, B, L, H, causal):
     return (p @ v).permute(0, 2, 1, 3).reshape(B * L, D)
 
 
-@pytest.fixture(params=[0, 1, 2, 5, 9, 13, 16, 29, 61, 125], ids=lambda v: f"attn_var{v}")
+@pytest.fixture(params=[0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 381], ids=lambda v: f"attn_var{v}")
 def attn_var(request):
     """Every attention forward variant (ce_set_attn_variant) against torch f32."""
     prev = _lib.lib().ce_set_attn_variant(request.param)
@@ -404,3 +404,30 @@ def test_layernorm(rows, D, bf16):
     ref = torch.nn.functional.layer_norm(x, (D,), w, b, 1e-5)
     err = (out.float() - ref).abs().max().item()
     assert err < (3e-2 if bf16 else 1e-4), err
+
+
+@pytest.mark.parametrize("s0", [6.0, -6.0, 0.0])
+@pytest.mark.parametrize("L", [577, 65, 129])
+def test_attention_cls_key_first(L, s0):
+    """Variant 381 (key 0 folded in before the key tiles, tiles over keys 1..L-1) with key 0 dominant
+    (s0 = +6: every query's score with it ~ +6 * 64 * 4 -> far past the fixed offset's +-64), far below
+    (-6) and ordinary: vs f32 attention and vs the default variant."""
+    B, H = 2, 4
+    g = torch.Generator(device="cpu").manual_seed(L + int(s0 * 10))
+    qkv = torch.randn(B * L, 3 * H * 64, generator=g) * 0.8
+    D = H * 64
+    if s0 != 0.0:
+        for b in range(B):
+            qkv[b * L:(b + 1) * L, 0:64] = qkv[b * L:(b + 1) * L, 0:64].abs() * 0 + 1.0   # head 0 queries
+            qkv[b * L, D:D + 64] = s0                                                        # key 0, head 0
+    qkv = qkv.to(torch.bfloat16).to(DEV)
+    ref = attn_ref(qkv, B, L, H, False)
+    prev = _lib.lib().ce_set_attn_variant(381)
+    try:
+        out = run_attn(qkv, B, L, H, False)
+    finally:
+        _lib.lib().ce_set_attn_variant(prev)
+    base = run_attn(qkv, B, L, H, False)
+    scale = max(1.0, ref.abs().max().item())
+    assert (out.float() - ref).abs().max().item() < 2e-2 * scale
+    assert (out.float() - base.float()).abs().max().item() < 2e-2 * scale
