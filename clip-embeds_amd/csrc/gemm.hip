@@ -143,7 +143,10 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        GEMM_VAR_SMALL_ONETILE = 8192,
        // (bits 14..18: SCHED 13 timing variants, gemm_db.hip)
        // the staged-residual kernel drains every epilogue store before the next tile's K-loop
-       GEMM_VAR_RHL_DRAIN = 1 << 19 };
+       GEMM_VAR_RHL_DRAIN = 1 << 19,
+       // staged-residual kernel: rows 6-7's residual loaded in the last K-tile (ABL bit 4); staged-row
+       // reads kept as single ds_read_b64 (ABL bit 5)
+       GEMM_VAR_RHL_EARLY67 = 1 << 20, GEMM_VAR_RHL_NOREAD2 = 1 << 21 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \
@@ -1818,10 +1821,17 @@ __device__ __forceinline__ float sum_lane_groups(float v) {
 //    K-tile 1 may stay in flight.
 // Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.
 // ABL: timing ablations (bit 0 no residual loads, bit 1 no stores; wrong outputs); bit 2: a K-tile's
-// operand DMAs spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD)
+// operand DMAs spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD); bit 4 (GEMM_VAR_RHL_EARLY67): the
+// residual of fragment rows 6-7 loaded into registers during the last K-tile's B3 (whose set-0
+// registers are free) instead of at the epilogue's start, so it is older than every store of the
+// epilogue; bit 5 (GEMM_VAR_RHL_NOREAD2): the staged-row reads as single ds_read_b64 (hipcc pairs
+// the hi / lo reads into ds_read2st64_b64, whose 32-bank 16-lane groups see a 2-way conflict on
+// this image)
 template <int ABL>
 __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     constexpr bool RSPREAD = (ABL & 4) != 0;
+    constexpr bool EARLY67 = (ABL & 16) != 0;
+    constexpr bool NOREAD2 = (ABL & 32) != 0;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1920,6 +1930,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     f32x4 acc[8][8];
     bf16x8 a0[8], b0[8], a1[8], b1[8];
     u32x4 rah[8], ral[8];                       // residual of fragment rows 4-5 (hi, lo planes)
+    u32x4 rbh[8], rbl[8];                       // rows 6-7 (EARLY67: from the last K-tile's B3)
     if constexpr ((ABL & 1) != 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) rah[j] = ral[j] = u32x4{0u, 0u, 0u, 0u};
@@ -2005,10 +2016,23 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();
+        int rpk6 = 0;
+        if constexpr (MODE == 2 && EARLY67) {
+            const int lnr = fresh_lane_id();
+            rpk6 = ((wm * 128 + 96 + (lnr & 15) + ((lnr >> 4) & 1) * 16) * (int)p.ldr + wn * 128 + (lnr >> 5) * 8) * 2;
+        }
 #pragma unroll
         for (int s2 = 0; s2 < 32; ++s2) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
+            if constexpr (MODE == 2 && EARLY67) {
+                // rows 6-7 of both planes, 16-B store layout (load_pair's), one load per 2 MFMAs
+                if (s2 & 1) {
+                    const int q = s2 >> 1;
+                    if (q < 8) rbh[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdH, rpk6 + q * 32, n0 * 2, 0));
+                    else rbl[q - 8] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdL, rpk6 + (q - 8) * 32, n0 * 2, 0));
+                }
+            }
             if constexpr (MODE == 0 && RSPREAD) {
                 // the other 6 DMAs of K-tile kt + 2 (buf's last reader was B1, before the first barrier)
                 if (s2 % 5 == 4) dma_k(buf, kt + 2, 10 + s2 / 5, voffA, voffW);
@@ -2098,9 +2122,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 l[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ls, vo + j * 32, 0, 0));
             }
         };
-        // (a) rows 6-7 (rows 4-5 arrived with the last K-tiles)
-        u32x4 rbh[8], rbl[8];
-        load_pair(rbh, rbl, 6);
+        // (a) rows 6-7 (rows 4-5 arrived with the last K-tiles; EARLY67: 6-7 too)
+        if constexpr (!EARLY67) load_pair(rbh, rbl, 6);
         const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
         const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
         int xo = ((fre + (fqe & 1) * 16) * ldo + nbase + (fqe >> 1) * 8) * 2;
@@ -2171,8 +2194,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
 #pragma unroll
             for (int r2 = 0; r2 < 2; ++r2) {
                 const int off = lr0 + (i0 + r2) * 16 * 512 + (c << 4) + (fqe & 1) * 8;
+                int offl = llo + off;
+                if constexpr (NOREAD2) asm volatile("" : "+v"(offl));   // keeps the two reads apart
                 const uint2 h = *reinterpret_cast<const uint2*>(smem + off);
-                const uint2 l = *reinterpret_cast<const uint2*>(smem + llo + off);
+                const uint2 l = *reinterpret_cast<const uint2*>(smem + offl);
                 const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
                 rr[r2] = make_float4(a.x, a.y, b.x, b.y);
             }
@@ -2639,7 +2664,14 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.stagger = gemm_stagger();
             plan_tail_rhl(p, nwg, w4pp_grid(nwg, p.onetile));
             const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
-            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && (gemm_variant() & GEMM_VAR_RHL_DRAIN))
+            const int ex = ((gemm_variant() & GEMM_VAR_RHL_EARLY67) ? 16 : 0) | ((gemm_variant() & GEMM_VAR_RHL_NOREAD2) ? 32 : 0);
+            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 16)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<20>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 32)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<36>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 48)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<52>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && (gemm_variant() & GEMM_VAR_RHL_DRAIN))
                 hipLaunchKernelGGL(gemm_w4_resid_hl<12>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
             else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
                 hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
