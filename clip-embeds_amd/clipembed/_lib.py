@@ -105,6 +105,7 @@ _SIGNATURES = {
     "ce_set_gemm_auto": (c_int, [c_int]),
     "ce_set_gemm_variant": (c_int, [c_int]),
     "ce_set_attn_variant": (c_int, [c_int]),
+    "ce_set_attn_bwd_variant": (c_int, [c_int]),
     "ce_set_fgemm_variant": (c_int, [c_int]),
     "ce_set_gemm_trace": (c_int, [c_void_p, c_int64]),
     "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),

@@ -2114,6 +2114,7 @@ int ce_gemm_path_counts(int64_t* counts, int n, int reset) {
     return CE_OK;
 }
 int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
+int ce_set_attn_bwd_variant(int v) { return ce::set_attn_bwd_variant(v); }
 int ce_set_gemm_splitk(int enable) { return ce::set_gemm_splitk(enable); }
 int ce_set_ln_fold(ce_handle* h, int enable, int* previous) {
     if (!h) return fail(CE_ERR_INVALID, "ce_set_ln_fold: null handle");

@@ -228,6 +228,7 @@ hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, 
 // attention backward (L <= 80): dqkv [B*L][3*H*64] from qkv (q pre-scaled), O, dO [B*L][H*64]
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
                                 int B, int L, int H, bool causal, hipStream_t s);
+int set_attn_bwd_variant(int v);   // 2 = transposed-read kernel (default), 1 = the transposed-copy kernel
 // token / positional embedding gradients from dx [B*ctx][D] (dtok fully overwritten)
 size_t embed_bwd_scratch_bytes(int B, int ctx, int D);
 hipError_t launch_embed_bwd(float* dtok, float* dpos, const float* dx, const int64_t* ids, int B, int ctx, int D,

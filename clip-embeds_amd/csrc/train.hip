@@ -369,6 +369,143 @@ __global__ __launch_bounds__(256) void attn_bwd_k(bf16_t* __restrict__ dqkv, con
 }
 
 // ---------------------------------------------------------------------------------------------
+// Attention backward, v2 (default; CE_ATTN_BWD=1 / ce_set_attn_bwd_variant(1) keeps attn_bwd_k): the
+// same arithmetic without the transposed LDS copies.  Every operand a product contracts over its
+// image's ROW index comes from ds_read_b64_tr_b16 on the row-major image (guide T10: lane 4q+p of a
+// 16-lane group addresses row r0 + q, columns c0 + 4p .. +3; lane i receives column c0 + i of the 4
+// rows), so q', k, v, dO are staged once with 16-B stores and P, dS once each: 73 KB of LDS instead
+// of 136 KB, two workgroups per CU.  Contractions over i / j run to K = 16 * ceil(L / 16) (80 at L = 77:
+// two 16x16x32 steps + one 16x16x16 step; rows L .. K-1 of every image are zero).
+constexpr int AB2_LP = 88;     // P / dS row stride (elements): K = 80 columns + pad
+__device__ __forceinline__ s16x4 tr4(const bf16_t* img, int ld, int r0, int c0, int lane) {
+    const int li = lane & 15;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (CE_LDS s16x4*)(img + (size_t)(r0 + (li >> 2)) * ld + c0 + 4 * (li & 3)));
+}
+// operand fragments of a 16-row (or column) block m0 of a product contracting over k:
+//   TR = false: image [m][k] (k contiguous);  TR = true: image [k][m] (m contiguous)
+template <bool TR>
+__device__ __forceinline__ bf16x8 frag8(const bf16_t* img, int ld, int m0, int k0, int lane) {
+    const int g = lane >> 4;
+    if constexpr (!TR) {
+        return *reinterpret_cast<const bf16x8*>(img + (size_t)(m0 + (lane & 15)) * ld + k0 + 8 * g);
+    } else {
+        const s16x4 lo = tr4(img, ld, k0 + 8 * g, m0, lane), hi = tr4(img, ld, k0 + 8 * g + 4, m0, lane);
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        return __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+}
+template <bool TR>
+__device__ __forceinline__ s16x4 frag4(const bf16_t* img, int ld, int m0, int k0, int lane) {
+    const int g = lane >> 4;
+    if constexpr (!TR) return *reinterpret_cast<const s16x4*>(img + (size_t)(m0 + (lane & 15)) * ld + k0 + 4 * g);
+    else return tr4(img, ld, k0 + 4 * g, m0, lane);
+}
+// C[16 x 16 tile at (m0, n0)] = sum_{k < K} Xop[m][k] Yop[n][k], K a multiple of 16; the lane's f32x4 =
+// rows m0 + 4 * (lane >> 4) + q, column n0 + (lane & 15)
+template <bool XT, bool YT>
+__device__ __forceinline__ f32x4 mfma_tile2(const bf16_t* X, int ldx, const bf16_t* Y, int ldy, int m0, int n0, int K,
+                                            int lane) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k0 = 0;
+    for (; k0 + 32 <= K; k0 += 32)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag8<XT>(X, ldx, m0, k0, lane), frag8<YT>(Y, ldy, n0, k0, lane),
+                                                      acc, 0, 0, 0);
+    if (k0 < K)
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(frag4<XT>(X, ldx, m0, k0, lane), frag4<YT>(Y, ldy, n0, k0, lane),
+                                                        acc, 0, 0, 0);
+    return acc;
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ qkv,
+                                                      const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                      const float* __restrict__ lse, int L, int H, int causal) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][AB_LD]
+    bf16_t* Ks = Qs + AB_L * AB_LD;
+    bf16_t* Vs = Ks + AB_L * AB_LD;
+    bf16_t* dOs = Vs + AB_L * AB_LD;
+    bf16_t* Ps = dOs + AB_L * AB_LD;                         // [80][AB2_LP]  P[i][j]
+    bf16_t* dSs = Ps + AB_L * AB2_LP;                        // [80][AB2_LP]  dS[i][j]
+    float* delta = reinterpret_cast<float*>(dSs + AB_L * AB2_LP);   // [80]
+    float* lrow = delta + AB_L;                                      // [80]
+
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int D = H * 64, ld = 3 * D;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nt = (L + 15) / 16, K = nt * 16;
+    if (tid < AB_L) lrow[tid] = tid < L ? lse[(size_t)bh * L + tid] : 0.f;
+    // q', k, v, dO rows (zero past L) + delta_i = dO_i . O_i
+    for (int e = tid; e < AB_L * 8; e += 256) {
+        const int i = e >> 3, c = (e & 7) * 8;
+        uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, g = q, o = q;
+        if (i < L) {
+            const size_t row = (size_t)(b * L + i);
+            q = *reinterpret_cast<const uint4*>(qkv + row * ld + h * 64 + c);
+            k = *reinterpret_cast<const uint4*>(qkv + row * ld + D + h * 64 + c);
+            v = *reinterpret_cast<const uint4*>(qkv + row * ld + 2 * D + h * 64 + c);
+            g = *reinterpret_cast<const uint4*>(dO + row * D + h * 64 + c);
+            o = *reinterpret_cast<const uint4*>(O + row * D + h * 64 + c);
+        }
+        *reinterpret_cast<uint4*>(Qs + i * AB_LD + c) = q;
+        *reinterpret_cast<uint4*>(Ks + i * AB_LD + c) = k;
+        *reinterpret_cast<uint4*>(Vs + i * AB_LD + c) = v;
+        *reinterpret_cast<uint4*>(dOs + i * AB_LD + c) = g;
+        const bf16_t* gs = reinterpret_cast<const bf16_t*>(&g);
+        const bf16_t* os = reinterpret_cast<const bf16_t*>(&o);
+        float part = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) part += bf2f(gs[t]) * bf2f(os[t]);
+        part += __shfl_xor(part, 1, 64);
+        part += __shfl_xor(part, 2, 64);
+        part += __shfl_xor(part, 4, 64);
+        if ((e & 7) == 0) delta[i] = part;
+    }
+    __syncthreads();
+    // per 16 x 16 tile: S = q' k^T -> P = exp2(S - lse) (masked) -> dP = dO V^T -> dS
+    for (int t = wave; t < nt * nt; t += 4) {
+        const int ti = t / nt, tj = t - ti * nt;
+        const f32x4 sv = mfma_tile2<false, false>(Qs, AB_LD, Ks, AB_LD, ti * 16, tj * 16, 64, lane);
+        const f32x4 dp = mfma_tile2<false, false>(dOs, AB_LD, Vs, AB_LD, ti * 16, tj * 16, 64, lane);
+        const int j = tj * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = ti * 16 + 4 * (lane >> 4) + q;
+            const bool ok = i < L && j < L && !(causal && j > i);
+            const float p = ok ? exp2f(sv[q] - lrow[i]) : 0.f;
+            const float ds = ok ? 0.69314718055994531f * p * (dp[q] - delta[i]) : 0.f;
+            Ps[i * AB2_LP + j] = f2bf(p);
+            dSs[i * AB2_LP + j] = f2bf(ds);
+        }
+    }
+    __syncthreads();
+    // dq'[i][d] = sum_j dS[i][j] k[j][d];  dk[j][d] = sum_i dS[i][j] q'[i][d];  dv[j][d] = sum_i P[i][j] dO[i][d]
+    for (int t = wave; t < 3 * nt * 4; t += 4) {
+        const int which = t / (nt * 4), tt = t - which * nt * 4;
+        const int m0 = (tt >> 2) * 16, n0 = (tt & 3) * 16;
+        f32x4 r;
+        if (which == 0) r = mfma_tile2<false, true>(dSs, AB2_LP, Ks, AB_LD, m0, n0, K, lane);
+        else if (which == 1) r = mfma_tile2<true, true>(dSs, AB2_LP, Qs, AB_LD, m0, n0, K, lane);
+        else r = mfma_tile2<true, true>(Ps, AB2_LP, dOs, AB_LD, m0, n0, K, lane);
+        const int col = which * D + h * 64 + n0 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = m0 + 4 * (lane >> 4) + q;
+            if (i < L) dqkv[(size_t)(b * L + i) * ld + col] = f2bf(r[q]);
+        }
+    }
+}
+
+int g_attn_bwd_var = -1;
+int attn_bwd_variant() {
+    if (g_attn_bwd_var < 0) {
+        const char* e = getenv("CE_ATTN_BWD");
+        g_attn_bwd_var = (e && atoi(e) == 1) ? 1 : 2;
+    }
+    return g_attn_bwd_var;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Token-embedding gradient, deterministic: (id, row) pairs sorted by id (stable radix sort), one
 // workgroup per run of equal ids sums its rows in row order.  Positional gradient: sum over batch.
 __global__ __launch_bounds__(256) void iota_ids_k(int* __restrict__ keys, int* __restrict__ vals,
@@ -653,6 +790,7 @@ hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, 
     return hipErrorInvalidValue;
 }
 
+constexpr size_t kAttnBwd2Lds = (size_t)(4 * AB_L * AB_LD + 2 * AB_L * AB2_LP) * 2 + (size_t)(2 * AB_L) * 4;
 constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * AB_LD + 3 * 64 * AB_LT + 3 * AB_L * AB_LT) * 2 + (size_t)(2 * AB_L) * 4;
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
                                 int B, int L, int H, bool causal, hipStream_t s) {
@@ -662,9 +800,26 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
         (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
         attr = true;
     }
+    if (attn_bwd_variant() == 2) {
+        static bool attr2 = false;
+        if (!attr2) {
+            (void)hipFuncSetAttribute((const void*)attn_bwd2_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kAttnBwd2Lds);
+            attr2 = true;
+        }
+        hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse, L,
+                           H, causal ? 1 : 0);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, lse, L, H,
                        causal ? 1 : 0);
     return hipGetLastError();
+}
+
+int set_attn_bwd_variant(int v) {
+    const int prev = attn_bwd_variant();
+    g_attn_bwd_var = v == 1 ? 1 : 2;
+    return prev;
 }
 
 size_t embed_bwd_scratch_bytes(int B, int ctx, int D) {

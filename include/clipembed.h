@@ -318,6 +318,11 @@ int ce_set_gemm_variant(int bits);
  * else restores the default (125).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
+/* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 2 = the
+ * transposed-read kernel (default: operands contracted over their image's row index come from
+ * ds_read_b64_tr_b16, 73 KB of LDS, two workgroups per CU), 1 = the kernel with transposed LDS copies
+ * (136 KB, one per CU).  Returns the previous setting. */
+int ce_set_attn_bwd_variant(int v);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
  * register-blocked 96 x 128 kernel (default; 16-B aligned operands with K % 4 == 0); 2 = as 1, and
  * for batched products of M <= 80 rows and N >= 192 (SPARC's T = 77 rows per sample) the 80 x 192
