@@ -777,6 +777,7 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
                        ce::current_gemm_sched() == 1;
     const int* seg = prune ? w.seg : nullptr;
     if (prune) CE_TRY(check_launch(ce::launch_text_pack(w.rows, w.seg, ids, B, L, s), "text_pack"));
+    else if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     h->seg_dev = nullptr;
     h->seg_host.clear();
     if (prune && h->timing && h->timing_only.empty()) {
@@ -787,7 +788,6 @@ int run_text(ce_handle* h, hipStream_t s, const TowerWs& w, const int64_t* ids, 
         HIP_TRY(hipStreamSynchronize(s));
         h->seg_dev = w.seg;
     }
-    else if (out_pooled) CE_TRY(check_launch(ce::launch_argmax_rows(w.rows, ids, B, L, s), "argmax"));
     if (use_fold) {
         CE_TRY(timed(h, s, "t_embed", 0.0, (double)B * L * D * (h->resid_hl ? 12.0 : 10.0), [&] {
             return ce::launch_text_embed_stats(w.x, w.xn, h->resid_hl ? w.xlo : nullptr, w.stats, ids,

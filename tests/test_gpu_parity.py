@@ -120,6 +120,37 @@ def test_pooled_prune_vs_oracle_ragged(small):
     assert cos_dist(pt, O.encode_text(sd, caps, cfg)) < COS_TOL
 
 
+@pytest.mark.parametrize("eots", [(13, 33), (40, 5, 60), (2, 2)])
+def test_pooled_text_packed_rows_every_caption(small, eots):
+    """Packed text rows (pooled-only encode_text): every caption of the batch, not only the first (whose
+    packed and unpacked rows coincide), matches the unpruned tokens call and the oracle; also with the
+    per-kernel profile pass on, which reads the packed offsets back (round-4 regression: that readback
+    displaced the pooled-row selection)."""
+    cfg = small.cfg
+    sd = W.synthetic_state_dict(cfg)
+    rng = np.random.default_rng(sum(eots))
+    caps = np.zeros((len(eots), 77), np.int64)
+    for i, e in enumerate(eots):
+        caps[i, 0], caps[i, e] = 49406, 49407
+        caps[i, 1:e] = rng.integers(1, 49000, e - 1)
+    ct = torch.from_numpy(caps)
+    ref = O.encode_text(sd, caps, cfg)
+    pt = small.encode_text(ct).cpu().numpy()
+    small.engine.set_timing(True)
+    try:
+        pt2 = small.encode_text(ct).cpu().numpy()
+    finally:
+        small.engine.set_timing(False)
+    small.output_text_tokens = True
+    try:
+        rt, _ = small.encode_text(ct)
+    finally:
+        small.output_text_tokens = False
+    rt = rt.cpu().numpy()
+    assert cos_dist(pt, rt) < 2e-5 and cos_dist(pt2, rt) < 2e-5
+    assert cos_dist(pt, ref) < COS_TOL
+
+
 def test_bf16_pixels(small):
     imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
     a = small.encode_image(imgs)
