@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     }
 }
 
-int g_attn_var = 125;
+int g_attn_var = 381;
 
 // One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
 // mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
@@ -734,7 +734,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
             case 9: CE_ATTN_LAUNCH(false, 9); break;
             case 13: CE_ATTN_LAUNCH(false, 13); break;
             case 1: CE_ATTN_LAUNCH(false, 1); break;
-            default: CE_ATTN_LAUNCH(false, 125); break;
+            default: CE_ATTN_LAUNCH(false, 381); break;
         }
     }
 #undef CE_ATTN_LAUNCH
@@ -745,7 +745,7 @@ int set_attn_variant(int var) {
     const int prev = g_attn_var;
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381)
-                     ? var : 125;
+                     ? var : 381;
     return prev;
 }
 

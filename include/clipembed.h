@@ -314,8 +314,10 @@ int ce_set_gemm_variant(int bits);
  * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
  * offset too (row sums checked from both sides), 64 = K/V DMAs through row-clipped buffer descriptors.
  * 128 = three K/V LDS slots (the next-but-one tile's DMA in flight; A/B only, measured slower: 3 workgroups
- * per CU instead of 4).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 253; anything
- * else restores the default (125).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
+ * per CU instead of 4), 256 = key 0 folded into O / l before the key tiles, which then cover keys 1..L-1
+ * (non-causal L with (L - 1) % 64 == 0: L = 577 runs 9 full tiles, no single-key masked tile; other L
+ * drop the bit).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 253, 381; anything else restores the
+ * default (381 = 125 + 256).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 2 = the

@@ -1,5 +1,5 @@
 """Attention variant 253 (bit 128: three K/V LDS slots, tile t+2's DMA in flight beside tile t+1's)
-vs the default variant 125 and the f32 reference, on the shapes of the image tower (L = 577, ragged
+vs variant 125 (the round-3 default) and the f32 reference, on the shapes of the image tower (L = 577, ragged
 last key tile), a short sequence and the dominant-key / wide-score cases."""
 import pytest
 import torch

@@ -3,6 +3,7 @@
 (guide §5.4 rule 24), random data.
 
     python tools/bench_gemm_epi.py --scheds 1,12 [--rounds 3] [--reps 10] [--only fc,qkv]
+    (':' also separates schedule tokens: tools/gpu_run.sh turns ',' into spaces)
 A schedule token: <sched>[g<groupm>][a<auto>][s<stagger>][v<variant bits>][n]  (n: split-K tail off; a0: auto policy off;\ns<k>: first-round stagger of k x s_sleep 127 for half the CUs).
 """
 import argparse
@@ -66,7 +67,7 @@ def main():
               # hi/lo residual stream (epi 3: resid and xb are [2][M][N] bf16 planes, no f32 output)
               "out_hl": (1024, 1024, 0, 3, True, False), "proj_hl": (1024, 4096, 0, 3, True, False)}
     if args.only:
-        shapes = {k: v for k, v in shapes.items() if k in args.only.split(",")}
+        shapes = {k: v for k, v in shapes.items() if k in args.only.replace(":", ",").split(",")}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     xw = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
     t0 = time.time()
@@ -96,7 +97,7 @@ def main():
     res = {}
     L = _lib.lib()
     for _ in range(args.rounds):
-        for tok in args.scheds.split(","):
+        for tok in args.scheds.replace(":", ",").split(","):
             sc, gm, auto, split, stag, var = parse(tok)
             L.ce_set_gemm_variant(var)
             L.ce_set_gemm_schedule(sc | (gm << 8) | (stag << 24))
