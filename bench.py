@@ -133,6 +133,21 @@ def load_traffic(tag):
         return None
 
 
+def load_mfma_busy(tag):
+    """Counter-based MFMA utilisation of `tag` (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE, one rocprofv3
+    --pmc pass over this bench; tools/summarize_mfma.py -> profiles/r04/mfma_busy.json), if measured."""
+    path = os.path.join(REPO, "profiles", "r04", "mfma_busy.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)["kernels"].get(tag)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not d:
+        return None
+    return {"mfma_busy": d["mfma_busy"], "clock_GHz": d["clock_GHz"], "frac_at_nominal": d["frac_at_nominal"],
+            "source": "profiles/r04/mfma_busy.json"}
+
+
 # ----------------------------------------------------------------------------------- workloads
 def pooled_prune_flops(cfg, on=True, eot=None):
     """FLOPs per pair NOT executed by pooled-only calls (ce_set_pooled_prune): the image tower's last
@@ -472,7 +487,9 @@ def main():
                     "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                     "traffic": load_traffic(top["name"]) if top["name"] in W.get("pmc_tags", ()) else None,
                     "avg_launch_ms": round(per_ms, 4),
-                    "flops_per_launch": top["flops"] / top["launches"]}
+                    "flops_per_launch": top["flops"] / top["launches"],
+                    # the same kernel's MFMA-pipe busy fraction from hardware counters (committed profile)
+                    "counters": load_mfma_busy(top["name"]) if args.workload == "clip" else None}
         else:
             ach = (top["bytes"] / top["launches"]) / (per_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": top["name"], "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
