@@ -88,9 +88,10 @@ def test_sparc_align_precomputed_embeddings_vs_oracle(models):
 
 @pytest.mark.parametrize("B,T,P,D", [(64, 77, 576, 768), (3, 5, 40, 128), (2, 77, 576, 1024)])
 def test_fgemm_variants_agree(models, B, T, P, D):
-    """The short-M 80 x 192 f32 GEMM (default for SPARC's similarity and grouping einsums,
-    pacl.py:460,472: v_mfma_f32_16x16x4_f32) and the register-blocked 96 x 128 kernel vs the 64 x 64
-    kernel, on the same inputs, and vs the oracle; ragged M / N / K tiles and D = 1024."""
+    """The register-blocked 96 x 128 f32 GEMM (the default for SPARC's similarity and grouping
+    einsums, pacl.py:460,472) and the selectable short-M 80 x 192 kernel (v_mfma_f32_16x16x4_f32,
+    ce_set_fgemm_variant(2), measured slower: DESIGN §6.11) vs the 64 x 64 kernel, on the same inputs,
+    and vs the oracle; ragged M / N / K tiles and D = 1024."""
     from clipembed import _lib
     m = models["sparc"]
     rng = np.random.default_rng(B * 7 + D)
