@@ -865,7 +865,7 @@ struct TrainWs {
     int* rows;
     float *pooled, *u, *f;
     // backward scratch
-    float *dres, *dxn, *dpool, *du, *pooledT, *colsum, *lnscr;
+    float *dres, *dxn, *dpool, *du, *pooledT, *colsum, *lnscr, *bpart;
     bf16_t *dres_b, *dA, *dB, *TA, *TB, *WT;
     float* part;
     void* emb;
@@ -906,7 +906,9 @@ size_t train_layout(const ce_handle* h, int B, TrainWs* w, char* base) {
     t.dpool = (float*)take((size_t)B * D * 4);
     t.du = (float*)take((size_t)B * E * 4);
     t.pooledT = (float*)take((size_t)B * D * 4);
-    t.colsum = (float*)take(ce::colsum_scratch_floats((int)M, (int)NX) * 4);
+    t.colsum = (float*)take(std::max(ce::colsum_scratch_floats((int)M, (int)NX),
+                                     ce::act_bwd_colsum_scratch_floats((int)M, F)) * 4);
+    t.bpart = (float*)take((size_t)B * 3 * D * 4);      // attention backward: per-caption in_proj bias sums
     t.lnscr = (float*)take(ce::ln_bwd_scratch_floats((int)M, D) * 4);
     t.dres_b = (bf16_t*)take(M * D * 2);
     t.dA = (bf16_t*)take(M * NX * 2);
@@ -1014,25 +1016,29 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         CE_TRY(timed(h, s, "t_d_pooled", 0.0, 0.0, [&] { return ce::launch_fgemm(fq, true, s); }));
     }
     HIP_TRY(hipMemsetAsync(w.dres, 0, (size_t)M * D * 4, s));
+    HIP_TRY(hipMemsetAsync(w.dres_b, 0, (size_t)M * D * 2, s));
+    // ln_final on the EOT rows; its dres rows are the top block's c_proj output gradient: the bf16 copy
+    // and that bias's column sums come out of the same kernel
+    const std::string top = "transformer.resblocks." + std::to_string(w.nl - 1) + ".";
     CE_TRY(timed(h, s, "t_ln_final_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[w.nl], w.dpool, D, W(h, "ln_final.weight"), w.rows, B, D,
                                           grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
-                                          w.lnscr, s); }));
+                                          w.lnscr, s, w.dres_b, grad_of(h, top + "mlp.c_proj.bias")); }));
     const float qs = ce::kAttnQScale;
     for (int l = w.nl - 1; l >= 0; --l) {
         const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
         const Blk k = block_ptrs(h, pfx);
         auto G = [&](const char* n) { return grad_of(h, pfx + n); };
         // ---- MLP: X[l+1] = XM + c_proj(act(c_fc(ln_2 XM)))  (transformer.py:235-239, 267) ----
-        CE_TRY(timed(h, s, "t_cast", 0.0, 0.0, [&] { return ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s); }));
-        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("mlp.c_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s); }));
+        // (dres_b and the c_proj bias gradient came out of the ln backward that produced dres)
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_proj", w.TA, Mp, w.TB, Mp, D, F, Mp, nullptr, 0, nullptr, G("mlp.c_proj.weight"), false,
                      w.part));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s); }));
         CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
-        CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] { return ce::launch_act(w.dA, w.pre[l], w.dA, (long)M * F, act, s); }));
-        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("mlp.c_fc.bias"), w.dA, false, F, M, F, 1.f, false, w.colsum, s); }));
+        CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] {
+            return ce::launch_act_bwd_colsum(w.dA, w.pre[l], w.dA, M, F, act, G("mlp.c_fc.bias"), w.colsum, s);
+        }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_fc", w.TA, Mp, w.TB, Mp, F, D, Mp, nullptr, 0, nullptr, G("mlp.c_fc.weight"), false,
@@ -1040,10 +1046,9 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s); }));
         CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, w.dxn, false, w.part));
         CE_TRY(timed(h, s, "t_ln_2_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
-                                              G("ln_2.bias"), true, false, w.lnscr, s); }));
+                                              G("ln_2.bias"), true, false, w.lnscr, s, w.dres_b,
+                                              G("attn.out_proj.bias")); }));
         // ---- attention: XM = X + out_proj(MHA(ln_1 X))  (transformer.py:242-255, 266) ----
-        CE_TRY(timed(h, s, "t_cast", 0.0, 0.0, [&] { return ce::launch_cast_bf16(w.dres_b, w.dres, (long)M * D, s); }));
-        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("attn.out_proj.bias"), w.dres, true, D, M, D, 1.f, false, w.colsum, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s); }));
         CE_TRY(tgemm(h, s, "dW_out", w.TA, Mp, w.TB, Mp, D, D, Mp, nullptr, 0, nullptr, G("attn.out_proj.weight"),
@@ -1051,11 +1056,10 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wout, false, D, D, D, D, s); }));
         CE_TRY(tgemm(h, s, "dX_out", w.dres_b, D, w.WT, D, M, D, D, nullptr, 0, nullptr, w.dB, true, w.part));
         CE_TRY(timed(h, s, "attn_bwd", 10.0 * B * H * (double)L * L * 64, 0.0, [&] {
-            return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, w.lse[l], B, L, H, true, s);
+            return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, w.lse[l], B, L, H, true, s,
+                                            G("attn.in_proj_bias"), w.bpart);
         }));
         // in_proj: the engine's q rows carry kAttnQScale, so d(master q rows) = qs * d(engine q rows)
-        CE_TRY(timed(h, s, "t_colsum", 0.0, 0.0, [&] { return ce::launch_colsum(G("attn.in_proj_bias"), w.dA, false, 3 * D, M, 3 * D, 1.f, false,
-                                              w.colsum, s); }));
         CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_bias"), D, qs, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s); }));
@@ -1064,8 +1068,11 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s); }));
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s); }));
         CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, w.dxn, false, w.part));
+        // (dres is now the gradient of X[l] = the c_proj output of block l - 1: its bf16 copy and that
+        // bias's column sums come out of this kernel)
+        float* below = l > 0 ? grad_of(h, "transformer.resblocks." + std::to_string(l - 1) + ".mlp.c_proj.bias") : nullptr;
         CE_TRY(timed(h, s, "t_ln_1_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[l], w.dxn, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
-                                              G("ln_1.bias"), true, false, w.lnscr, s); }));
+                                              G("ln_1.bias"), true, false, w.lnscr, s, w.dres_b, below); }));
     }
     // token / positional embeddings (model.py:286-288)
     CE_TRY(timed(h, s, "t_embed_bwd", 0.0, 0.0, [&] { return ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),

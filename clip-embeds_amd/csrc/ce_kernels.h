@@ -218,16 +218,23 @@ hipError_t launch_transpose_f32(float* out, long ldo, const float* in, long ldi,
 long colsum_scratch_floats(int M, int N);
 hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M, int N, float scale, bool accumulate,
                          float* scratch, hipStream_t s);
-// LayerNorm backward (eps 1e-5): dres[xrow] (+)= dx; dw, db (+)= column sums (scratch >= ln_bwd_scratch_floats)
+// LayerNorm backward (eps 1e-5): dres[xrow] (+)= dx; dw, db (+)= column sums (scratch >= ln_bwd_scratch_floats);
+// dres_b (nullable): bf16 copy of the updated dres rows; dsum (nullable): = column sums of the updated dres rows
 long ln_bwd_scratch_floats(int n, int D);
 hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
                          int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
-                         hipStream_t s);
+                         hipStream_t s, bf16_t* dres_b = nullptr, float* dsum = nullptr);
+// out = dh * act'(pre) over [M][N] bf16 and dbias = column sums of out (scratch >= act_bwd_colsum_scratch_floats)
+long act_bwd_colsum_scratch_floats(int M, int N);
+hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* dh, int M, int N, int act, float* dbias,
+                                 float* scratch, hipStream_t s);
 // dh == nullptr: out = act(pre); else out = dh * act'(pre).  bf16, n % 8 == 0.
 hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s);
 // attention backward (L <= 80): dqkv [B*L][3*H*64] from qkv (q pre-scaled), O, dO [B*L][H*64]
+// dbias (nullable): = column sums of dqkv over all rows (the in_proj bias gradient); bpart: [B][3*H*64] f32 scratch
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
-                                int B, int L, int H, bool causal, hipStream_t s);
+                                int B, int L, int H, bool causal, hipStream_t s, float* dbias = nullptr,
+                                float* bpart = nullptr);
 int set_attn_bwd_variant(int v);   // 2 = transposed-read kernel (default), 1 = the transposed-copy kernel
 // token / positional embedding gradients from dx [B*ctx][D] (dtok fully overwritten)
 size_t embed_bwd_scratch_bytes(int B, int ctx, int D);

@@ -133,18 +133,22 @@ __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, 
 //   xh = (x - mu) * rstd;  g = dy * w;  dx = rstd * (g - mean(g) - xh * mean(g * xh))
 //   dres[row] (+)= dx;  part_w[blk] += dy * xh;  part_b[blk] += dy
 // rows != null: x and dres rows are rows[i] (EOT pooling), dy row is i.
+// dres_b (nullable): bf16 copy of the updated dres row (the next dX GEMM's operand); part_r (nullable):
+// per-block column sums of the updated dres (the bias gradient of the GEMM that produced the residual:
+// c_proj / out_proj, as the colsum of dres, fused)
 constexpr int LNB_ROWS = 16;   // rows per block (partial dw/db per block)
 template <int NC>
 __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const float* __restrict__ x,
                                                 const float* __restrict__ dy, long ldy, const float* __restrict__ w,
                                                 const int* __restrict__ rows, int n, float* __restrict__ part_w,
-                                                float* __restrict__ part_b, int accumulate) {
+                                                float* __restrict__ part_b, int accumulate, bf16_t* __restrict__ dres_b,
+                                                float* __restrict__ part_r) {
     constexpr int D = NC * 256;
-    __shared__ float red[2][4][D];
+    __shared__ float red[3][4][D];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float4 aw[NC], ab[NC];
+    float4 aw[NC], ab[NC], ar[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) aw[c] = ab[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = 0; c < NC; ++c) aw[c] = ab[c] = ar[c] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int r0 = blockIdx.x * LNB_ROWS;
     for (int i = r0 + wave; i < min(n, r0 + LNB_ROWS); i += 4) {
         const long xr = rows ? rows[i] : i;
@@ -189,6 +193,13 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const 
                 dx.x += old.x; dx.y += old.y; dx.z += old.z; dx.w += old.w;
             }
             *o = dx;
+            ar[c].x += dx.x; ar[c].y += dx.y; ar[c].z += dx.z; ar[c].w += dx.w;
+            if (dres_b) {
+                uint2 hb;
+                hb.x = (uint32_t)f2bf(dx.x) | ((uint32_t)f2bf(dx.y) << 16);
+                hb.y = (uint32_t)f2bf(dx.z) | ((uint32_t)f2bf(dx.w) << 16);
+                *reinterpret_cast<uint2*>(dres_b + xr * D + e) = hb;
+            }
         }
     }
 #pragma unroll
@@ -196,11 +207,13 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const 
         const int e = c * 256 + lane * 4;
         *reinterpret_cast<float4*>(&red[0][wave][e]) = aw[c];
         *reinterpret_cast<float4*>(&red[1][wave][e]) = ab[c];
+        *reinterpret_cast<float4*>(&red[2][wave][e]) = ar[c];
     }
     __syncthreads();
     for (int e = threadIdx.x; e < D; e += 256) {
         part_w[(size_t)blockIdx.x * D + e] = (red[0][0][e] + red[0][1][e]) + (red[0][2][e] + red[0][3][e]);
         part_b[(size_t)blockIdx.x * D + e] = (red[1][0][e] + red[1][1][e]) + (red[1][2][e] + red[1][3][e]);
+        if (part_r) part_r[(size_t)blockIdx.x * D + e] = (red[2][0][e] + red[2][1][e]) + (red[2][2][e] + red[2][3][e]);
     }
 }
 
@@ -235,6 +248,46 @@ __global__ __launch_bounds__(256) void act_k(bf16_t* __restrict__ out, const bf1
         os[k] = f2bf(y);
     }
     reinterpret_cast<uint4*>(out)[i] = ov;
+}
+
+// Activation backward fused with the bias gradient of the GEMM that produced `pre` (c_fc): out = dh *
+// act'(pre) (in place allowed), part[blk][n] = sum over the block's rows of the bf16-rounded out (the
+// values the old separate colsum read).  Block = 64 column chunks of 8 (512 columns) x 4 row lanes,
+// rows [blk * cs, (blk + 1) * cs); fixed summation order.  N % 8 == 0.
+template <int ACT>
+__global__ __launch_bounds__(256) void act_bwd_colsum_k(bf16_t* out, const bf16_t* __restrict__ pre,
+                                                        const bf16_t* dh, int M, int N, int cs,
+                                                        float* __restrict__ part) {
+    __shared__ float red[4][512];
+    const int c8 = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    const int n = blockIdx.x * 512 + c8 * 8;
+    const int m0 = blockIdx.y * cs, m1 = min(M, m0 + cs);
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (n < N) {
+        for (int m = m0 + r4; m < m1; m += 4) {
+            const size_t o = (size_t)m * N + n;
+            const uint4 pv = *reinterpret_cast<const uint4*>(pre + o);
+            const uint4 dv = *reinterpret_cast<const uint4*>(dh + o);
+            const bf16_t* ps = reinterpret_cast<const bf16_t*>(&pv);
+            const bf16_t* ds = reinterpret_cast<const bf16_t*>(&dv);
+            uint4 ov;
+            bf16_t* os = reinterpret_cast<bf16_t*>(&ov);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float x = bf2f(ps[k]);
+                os[k] = f2bf(bf2f(ds[k]) * (ACT == ACT_QGELU ? qgelu_grad(x) : gelu_grad(x)));
+                a[k] += bf2f(os[k]);
+            }
+            *reinterpret_cast<uint4*>(out + o) = ov;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[r4][c8 * 8 + k] = a[k];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 512; e += 256) {
+        const int nn = blockIdx.x * 512 + e;
+        if (nn < N) part[(size_t)blockIdx.y * N + nn] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -417,9 +470,13 @@ __device__ __forceinline__ f32x4 mfma_tile2(const bf16_t* X, int ldx, const bf16
     return acc;
 }
 
+// bpart (nullable): [B][3D] per-caption column sums of the bf16-rounded dq' | dk | dv (the in_proj
+// bias gradient before the caller's sum over captions): wave w owns column block tj = w of every
+// product (t = w, w + 4, ... walks ti for fixed tj), so each column is summed in one fixed order
 __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ qkv,
                                                       const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                      const float* __restrict__ lse, int L, int H, int causal) {
+                                                      const float* __restrict__ lse, int L, int H, int causal,
+                                                      float* __restrict__ bpart) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][AB_LD]
     bf16_t* Ks = Qs + AB_L * AB_LD;
@@ -480,6 +537,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv,
     }
     __syncthreads();
     // dq'[i][d] = sum_j dS[i][j] k[j][d];  dk[j][d] = sum_i dS[i][j] q'[i][d];  dv[j][d] = sum_i P[i][j] dO[i][d]
+    float csum = 0.f;
     for (int t = wave; t < 3 * nt * 4; t += 4) {
         const int which = t / (nt * 4), tt = t - which * nt * 4;
         const int m0 = (tt >> 2) * 16, n0 = (tt & 3) * 16;
@@ -491,7 +549,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int i = m0 + 4 * (lane >> 4) + q;
-            if (i < L) dqkv[(size_t)(b * L + i) * ld + col] = f2bf(r[q]);
+            if (i < L) {
+                const bf16_t v = f2bf(r[q]);
+                dqkv[(size_t)(b * L + i) * ld + col] = v;
+                csum += bf2f(v);
+            }
+        }
+        if (bpart && (tt >> 2) == nt - 1) {       // last row tile of this column block: reduce, store
+            csum += __shfl_xor(csum, 16, 64);
+            csum += __shfl_xor(csum, 32, 64);
+            if (lane < 16) bpart[(size_t)b * 3 * D + col] = csum;
+            csum = 0.f;
         }
     }
 }
@@ -756,24 +824,50 @@ hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M
 
 long ln_bwd_scratch_floats(int n, int D) {
     const int nb = (n + LNB_ROWS - 1) / LNB_ROWS;
-    return 2L * nb * D + colsum_scratch_floats(nb, D);
+    return 3L * nb * D + colsum_scratch_floats(nb, D);
 }
 hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
                          int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
-                         hipStream_t s) {
+                         hipStream_t s, bf16_t* dres_b, float* dsum) {
     if (n <= 0) return hipSuccess;
     const int nb = (n + LNB_ROWS - 1) / LNB_ROWS;
     float* pw = scratch;
     float* pb = scratch + (size_t)nb * D;
+    float* pr = dsum ? pb + (size_t)nb * D : nullptr;
     const int acc = accumulate_dx ? 1 : 0;
-    if (D == 768) hipLaunchKernelGGL(ln_bwd_k<3>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
-    else if (D == 1024) hipLaunchKernelGGL(ln_bwd_k<4>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
-    else if (D == 512) hipLaunchKernelGGL(ln_bwd_k<2>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc);
+#define CE_LNB(NC) hipLaunchKernelGGL(ln_bwd_k<NC>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc, \
+                                      dres_b, pr)
+    if (D == 768) CE_LNB(3);
+    else if (D == 1024) CE_LNB(4);
+    else if (D == 512) CE_LNB(2);
     else return hipErrorInvalidValue;
-    float* cscr = pb + (size_t)nb * D;
+#undef CE_LNB
+    float* cscr = pb + 2 * (size_t)nb * D;
     hipError_t e = launch_colsum(dw, pw, true, D, nb, D, 1.0f, accumulate_dwb, cscr, s);
     if (e == hipSuccess) e = launch_colsum(db, pb, true, D, nb, D, 1.0f, accumulate_dwb, cscr, s);
+    if (e == hipSuccess && dsum) e = launch_colsum(dsum, pr, true, D, nb, D, 1.0f, false, cscr, s);
     return e;
+}
+
+int act_colsum_chunk(int M, int N) {
+    const int colblocks = (N + 511) / 512;
+    const int target = std::max(1, 1536 / colblocks);
+    return std::max(16, (M + target - 1) / target);
+}
+long act_bwd_colsum_scratch_floats(int M, int N) {
+    return (long)((M + act_colsum_chunk(M, N) - 1) / act_colsum_chunk(M, N)) * N;
+}
+hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* dh, int M, int N, int act, float* dbias,
+                                 float* scratch, hipStream_t s) {
+    if (N % 8 || M <= 0) return hipErrorInvalidValue;
+    const int cs = act_colsum_chunk(M, N);
+    const int nb = (M + cs - 1) / cs;
+    const dim3 grid((unsigned)((N + 511) / 512), (unsigned)nb);
+    if (act == ACT_GELU) hipLaunchKernelGGL(act_bwd_colsum_k<ACT_GELU>, grid, dim3(256), 0, s, out, pre, dh, M, N, cs, scratch);
+    else if (act == ACT_QGELU) hipLaunchKernelGGL(act_bwd_colsum_k<ACT_QGELU>, grid, dim3(256), 0, s, out, pre, dh, M, N, cs, scratch);
+    else return hipErrorInvalidValue;
+    hipLaunchKernelGGL(colsum_finish_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, dbias, scratch, nb, N, 1.0f, 0);
+    return hipGetLastError();
 }
 
 hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s) {
@@ -793,7 +887,7 @@ hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, 
 constexpr size_t kAttnBwd2Lds = (size_t)(4 * AB_L * AB_LD + 2 * AB_L * AB2_LP) * 2 + (size_t)(2 * AB_L) * 4;
 constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * AB_LD + 3 * 64 * AB_LT + 3 * AB_L * AB_LT) * 2 + (size_t)(2 * AB_L) * 4;
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
-                                int B, int L, int H, bool causal, hipStream_t s) {
+                                int B, int L, int H, bool causal, hipStream_t s, float* dbias, float* bpart) {
     if (L <= 0 || L > AB_L || B <= 0 || !lse) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
@@ -808,11 +902,15 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
             attr2 = true;
         }
         hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse, L,
-                           H, causal ? 1 : 0);
+                           H, causal ? 1 : 0, dbias ? bpart : nullptr);
+        if (dbias)   // in_proj bias gradient: the captions' column sums, fixed order
+            hipLaunchKernelGGL(colsum_finish_k, dim3((unsigned)((3 * H * 64 + 63) / 64)), dim3(256), 0, s, dbias, bpart,
+                               B, 3 * H * 64, 1.0f, 0);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, lse, L, H,
                        causal ? 1 : 0);
+    if (dbias) return launch_colsum(dbias, dqkv, false, 3 * H * 64, B * L, 3 * H * 64, 1.0f, false, bpart, s);
     return hipGetLastError();
 }
 
