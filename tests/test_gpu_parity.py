@@ -151,6 +151,23 @@ def test_pooled_text_packed_rows_every_caption(small, eots):
     assert cos_dist(pt, ref) < COS_TOL
 
 
+def test_text_width_outside_the_fold_kernel():
+    """A text width the LN-fold entry kernel does not cover (1536: D % 64 == 0 but not one of its
+    256/512/768/1024/1280 instantiations) runs the unfolded text tower instead of failing
+    (round-3 advisor finding), within 1e-3 cosine of the oracle."""
+    import dataclasses
+    base = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    cfg = dataclasses.replace(base, name="text-1536", text=dataclasses.replace(base.text, width=1536, heads=24,
+                                                                                mlp_width=6144))
+    sd = W.synthetic_state_dict(cfg)
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(sd)
+    m.to("cuda")
+    caps = W.synthetic_captions(3, seed=91)
+    got = m.encode_text(torch.from_numpy(caps)).cpu().numpy()
+    assert cos_dist(got, O.encode_text(sd, caps, cfg)) < COS_TOL
+
+
 def test_bf16_pixels(small):
     imgs = torch.from_numpy(W.synthetic_images(2, seed=1000))
     a = small.encode_image(imgs)
