@@ -365,6 +365,12 @@ def main():
                     help="run every tower's last block for all rows (A/B of ce_set_pooled_prune)")
     ap.add_argument("--no-every-row", action="store_true",
                     help="skip the second timed leg with the pooled prune off (`every_row` in the JSON line)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank code path with every rank on one device, --share-device)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsal of the N > 1 path on a one-GPU box; needs gloo: "
+                         "RCCL runs one rank per device)")
     ap.add_argument("--gemm-stagger", type=int, default=-1,
                     help="first-round stagger of the persistent residual GEMMs (x s_sleep 127, odd slots; A/B)")
     args = ap.parse_args()
@@ -377,10 +383,17 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if args.share_device and args.dist_backend != "gloo":
+        log("error: --share-device needs --dist-backend gloo (RCCL runs one rank per device)")
+        sys.exit(2)
+    dev_index = 0 if args.share_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     if args.attn_var >= 0:
         from clipembed import _lib
@@ -517,6 +530,9 @@ def main():
         cpu = cpu_baseline(W["sd"], W["cfg"], args.cpu_batch)
         cpu["vs_gpu"] = round(value / cpu["value"], 1)
 
+    if world > 1:
+        W["config"]["dist_backend"] = args.dist_backend + (" (every rank on cuda:0: rehearsal, not a scaling number)"
+                                                           if args.share_device else "")
     out = {
         "metric": W["metric"],
         "value": round(value, 2),
