@@ -107,6 +107,9 @@ _SIGNATURES = {
     "ce_set_attn_variant": (c_int, [c_int]),
     "ce_set_attn_bwd_variant": (c_int, [c_int]),
     "ce_set_fgemm_variant": (c_int, [c_int]),
+    "ce_kernel_gemm_tn_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
+                                       c_int64, c_int, c_float]),
+    "ce_set_train_dw_tn": (c_int, [c_int]),
     "ce_set_gemm_trace": (c_int, [c_void_p, c_int64]),
     "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -963,6 +964,28 @@ int tgemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long ld
     return timed(h, s, tag, 2.0 * M * N * K, 0.0, [&] { return ce::launch_gemm(p, act, out_bf16, s); });
 }
 
+// weight gradients by the MN-major GEMM (gemm_tn.hip) or, 0, by transposed copies + the forward GEMM
+int g_dw_tn = -1;
+bool dw_tn() {
+    if (g_dw_tn < 0) {
+        const char* e = std::getenv("CE_TRAIN_DW_TN");
+        g_dw_tn = e ? (std::atoi(e) != 0) : 1;
+    }
+    return g_dw_tn != 0;
+}
+
+// dW[M][N] = scale_m * sum over the T token rows of A[t][m] B[t][n]  (row-major activations in place)
+int tgemm_tn(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M,
+             int N, int T, float* out, float* part, int scale_rows = 0, float scale = 1.f) {
+    ce::TnParams p{};
+    p.A = A; p.lda = lda; p.B = B; p.ldb = ldb;
+    p.M = M; p.N = N; p.K = T;
+    p.C = out; p.ldc = N;
+    p.part = part; p.part_elems = part ? ce::kGemmPartElems : 0;
+    p.scale_rows = scale_rows; p.scale = scale;
+    return timed(h, s, tag, 2.0 * M * N * T, 0.0, [&] { return ce::launch_gemm_tn(p, s); });
+}
+
 // text forward keeping every activation the backward needs (open_clip encode_text, model.py:283-301)
 int run_text_train(ce_handle* h, hipStream_t s, TrainWs& w, const int64_t* ids) {
     const ce_config& c = h->cfg;
@@ -1024,35 +1047,49 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
                                           grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
                                           w.lnscr, s, w.dres_b, grad_of(h, top + "mlp.c_proj.bias")); }));
     const float qs = ce::kAttnQScale;
+    // MN-major dW GEMMs: widths that are multiples of 256 (ViT-B/L text towers: 512, 768)
+    const bool tn = dw_tn() && D % 256 == 0 && F % 256 == 0;
     for (int l = w.nl - 1; l >= 0; --l) {
         const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
         const Blk k = block_ptrs(h, pfx);
         auto G = [&](const char* n) { return grad_of(h, pfx + n); };
         // ---- MLP: X[l+1] = XM + c_proj(act(c_fc(ln_2 XM)))  (transformer.py:235-239, 267) ----
         // (dres_b and the c_proj bias gradient came out of the ln backward that produced dres)
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s); }));
-        CE_TRY(tgemm(h, s, "dW_proj", w.TA, Mp, w.TB, Mp, D, F, Mp, nullptr, 0, nullptr, G("mlp.c_proj.weight"), false,
-                     w.part));
+        if (tn) {
+            CE_TRY(tgemm_tn(h, s, "dW_proj", w.dres_b, D, w.hh[l], F, D, F, M, G("mlp.c_proj.weight"), w.part));
+        } else {
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.hh[l], false, F, M, F, Mp, s); }));
+            CE_TRY(tgemm(h, s, "dW_proj", w.TA, Mp, w.TB, Mp, D, F, Mp, nullptr, 0, nullptr, G("mlp.c_proj.weight"), false,
+                         w.part));
+        }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s); }));
         CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
         CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] {
             return ce::launch_act_bwd_colsum(w.dA, w.pre[l], w.dA, M, F, act, G("mlp.c_fc.bias"), w.colsum, s);
         }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s); }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s); }));
-        CE_TRY(tgemm(h, s, "dW_fc", w.TA, Mp, w.TB, Mp, F, D, Mp, nullptr, 0, nullptr, G("mlp.c_fc.weight"), false,
-                     w.part));
+        if (tn) {
+            CE_TRY(tgemm_tn(h, s, "dW_fc", w.dA, F, w.xn2[l], D, F, D, M, G("mlp.c_fc.weight"), w.part));
+        } else {
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, F, M, F, Mp, s); }));
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn2[l], false, D, M, D, Mp, s); }));
+            CE_TRY(tgemm(h, s, "dW_fc", w.TA, Mp, w.TB, Mp, F, D, Mp, nullptr, 0, nullptr, G("mlp.c_fc.weight"), false,
+                         w.part));
+        }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s); }));
         CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, w.dxn, false, w.part));
         CE_TRY(timed(h, s, "t_ln_2_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
                                               G("ln_2.bias"), true, false, w.lnscr, s, w.dres_b,
                                               G("attn.out_proj.bias")); }));
         // ---- attention: XM = X + out_proj(MHA(ln_1 X))  (transformer.py:242-255, 266) ----
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s); }));
-        CE_TRY(tgemm(h, s, "dW_out", w.TA, Mp, w.TB, Mp, D, D, Mp, nullptr, 0, nullptr, G("attn.out_proj.weight"),
-                     false, w.part));
+        if (tn) {
+            CE_TRY(tgemm_tn(h, s, "dW_out", w.dres_b, D, w.att[l], D, D, D, M, G("attn.out_proj.weight"), w.part));
+        } else {
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dres, true, D, M, D, Mp, s); }));
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.att[l], false, D, M, D, Mp, s); }));
+            CE_TRY(tgemm(h, s, "dW_out", w.TA, Mp, w.TB, Mp, D, D, Mp, nullptr, 0, nullptr, G("attn.out_proj.weight"),
+                         false, w.part));
+        }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wout, false, D, D, D, D, s); }));
         CE_TRY(tgemm(h, s, "dX_out", w.dres_b, D, w.WT, D, M, D, D, nullptr, 0, nullptr, w.dB, true, w.part));
         CE_TRY(timed(h, s, "attn_bwd", 10.0 * B * H * (double)L * L * 64, 0.0, [&] {
@@ -1061,11 +1098,16 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         }));
         // in_proj: the engine's q rows carry kAttnQScale, so d(master q rows) = qs * d(engine q rows)
         CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_bias"), D, qs, s); }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s); }));
-        CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s); }));
-        CE_TRY(tgemm(h, s, "dW_qkv", w.TA, Mp, w.TB, Mp, 3 * D, D, Mp, nullptr, 0, nullptr, G("attn.in_proj_weight"),
-                     false, w.part));
-        CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s); }));
+        if (tn) {      // (the q rows' kAttnQScale applied by the split-K fixup)
+            CE_TRY(tgemm_tn(h, s, "dW_qkv", w.dA, 3 * D, w.xn1[l], D, 3 * D, D, M, G("attn.in_proj_weight"), w.part, D,
+                            qs));
+        } else {
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TA, Mp, w.dA, false, 3 * D, M, 3 * D, Mp, s); }));
+            CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.TB, Mp, w.xn1[l], false, D, M, D, Mp, s); }));
+            CE_TRY(tgemm(h, s, "dW_qkv", w.TA, Mp, w.TB, Mp, 3 * D, D, Mp, nullptr, 0, nullptr, G("attn.in_proj_weight"),
+                         false, w.part));
+            CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s); }));
+        }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s); }));
         CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, w.dxn, false, w.part));
         // (dres is now the gradient of X[l] = the c_proj output of block l - 1: its bf16 copy and that
@@ -2122,6 +2164,25 @@ int ce_gemm_path_counts(int64_t* counts, int n, int reset) {
 }
 int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule); }
 int ce_set_attn_bwd_variant(int v) { return ce::set_attn_bwd_variant(v); }
+int ce_set_train_dw_tn(int on) {
+    const int prev = dw_tn() ? 1 : 0;
+    g_dw_tn = on ? 1 : 0;
+    return prev;
+}
+int ce_kernel_gemm_tn_bf16(void* stream, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
+                           float* C, int64_t ldc, int scale_rows, float scale) {
+    if (!A || !B || !C) return fail(CE_ERR_INVALID, "ce_kernel_gemm_tn_bf16: null argument");
+    if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || lda < M || ldb < N || ldc < N || lda % 8 || ldb % 8 ||
+        ldc % 4)
+        return fail(CE_ERR_INVALID, "ce_kernel_gemm_tn_bf16: need M, N multiples of 256, K > 0, lda >= M, ldb >= N, "
+                    "ldc >= N (lda, ldb % 8 == 0, ldc % 4 == 0); got M %d N %d K %d", M, N, K);
+    ce::TnParams p{};
+    p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+    p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
+    p.part = ce::gemm_kernel_api_workspace(&p.part_elems);
+    p.scale_rows = scale_rows; p.scale = scale;
+    return check_launch(ce::launch_gemm_tn(p, (hipStream_t)stream), "gemm_tn");
+}
 int ce_set_gemm_splitk(int enable) { return ce::set_gemm_splitk(enable); }
 int ce_set_ln_fold(ce_handle* h, int enable, int* previous) {
     if (!h) return fail(CE_ERR_INVALID, "ce_set_ln_fold: null handle");

@@ -82,6 +82,22 @@ void set_gemm_trace(unsigned long long* buf, long n);   // diagnostics: per-bloc
 float* gemm_kernel_api_workspace(long* elems);   // per-device partial-tile buffer (kernel-level API)
 constexpr long kGemmPartElems = 256L * 256 * 256;   // partial-tile workspace a handle provides (64 MB)
 
+// Weight-gradient GEMM with MN-major operands (gemm_tn.hip): C[m][n] = scale_m * sum_k A[k][m] B[k][n]
+//   A [K][lda], B [K][ldb] bf16 (row-major activations, reduction down their rows), C [M][ldc] f32;
+//   scale_m = scale for m < scale_rows else 1.  M % 256 == 0, N % 256 == 0, 16-B aligned rows.
+//   part (nullable, part_elems floats): split-K partial tiles; null = one workgroup per tile.
+struct TnParams {
+    const bf16_t* A; long lda;
+    const bf16_t* B; long ldb;
+    int M, N, K;
+    float* C; long ldc;
+    float* part = nullptr; long part_elems = 0;
+    int split = 1;                       // set by the launcher
+    int scale_rows = 0; float scale = 1.f;
+};
+hipError_t launch_gemm_tn(const TnParams& p, hipStream_t s);
+int gemm_tn_split(int M, int N, int K, long part_elems);   // the K-split launch_gemm_tn picks (0: bad shape)
+
 // Multi-head attention over a packed QKV activation.
 //   qkv [B*L][3*D] bf16 (q | k | v, head h at columns h*64 .. h*64+63 of each part)
 //   out [B*L][D]   bf16 (heads concatenated), softmax(q k^T / sqrt(64) [+ causal]) v

@@ -325,6 +325,16 @@ int ce_set_attn_variant(int var);
  * ds_read_b64_tr_b16, 73 KB of LDS, two workgroups per CU), 1 = the kernel with transposed LDS copies
  * (136 KB, one per CU).  Returns the previous setting. */
 int ce_set_attn_bwd_variant(int v);
+/* Weight-gradient GEMM with MN-major operands: C[m][n] = scale_m * sum_k A[k][m] B[k][n]
+ * with A [K][lda], B [K][ldb] bf16 row-major (the activations of a linear layer's input and output
+ * gradient, reduction over their rows), C [M][ldc] f32, scale_m = scale for m < scale_rows else 1.
+ * M % 256 == 0, N % 256 == 0, lda >= M, ldb >= N (multiples of 8), 16-B aligned.  The text-tower
+ * backward's dW of in_proj / out_proj / c_fc / c_proj (autograd of transformer.py:228-239). */
+int ce_kernel_gemm_tn_bf16(void* stream, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,
+                           float* C, int64_t ldc, int scale_rows, float scale);
+/* Text-tower training: weight gradients by the MN-major GEMM above (1, default) or by transposed
+ * operand copies and the forward GEMM (0, the round-3 path).  Returns the previous setting.  For A/B. */
+int ce_set_train_dw_tn(int on);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
  * register-blocked 96 x 128 kernel (default; 16-B aligned operands with K % 4 == 0); 2 = as 1, and
  * for batched products of M <= 80 rows and N >= 192 (SPARC's T = 77 rows per sample) the 80 x 192

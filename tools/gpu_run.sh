@@ -4,6 +4,7 @@
 #   gputests                               the whole -m gpu suite
 #   smoke                                  __graft_entry__.smoke()
 #   bench:<bench.py args, comma-separated> one bench.py run (JSON line -> gpurun_out/TAG_benchN.log)
+#   envbench:<VAR=VAL>,<bench.py args>    one bench.py run with one environment setting (A/B)
 #   rocprof:<bench.py args>                rocprofv3 --kernel-trace --stats of one bench.py run
 #   clock:<bench.py args>                  GRBM_GUI_ACTIVE pass (effective clock per kernel)
 #   pmc:<counter>,<bench.py args>          one --pmc pass with one counter over a short bench run
@@ -26,6 +27,8 @@ for step in "$@"; do
                > gpurun_out/${TAG}_gputests.log 2>&1 ;;
     smoke)   timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     bench)   timeout -k 10 400 python -u bench.py $args > gpurun_out/${TAG}_bench$n.log 2>&1 ;;
+    envbench) ev=${args%% *}; rest=${args#* }
+             timeout -k 10 400 env $ev python -u bench.py $rest > gpurun_out/${TAG}_bench$n.log 2>&1 ;;
     rocprof) timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$n -o run --output-format csv -- \
                python3 -u bench.py --no-cpu-baseline $args > gpurun_out/${TAG}_prof$n.log 2>&1 ;;
     clock)   timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/${TAG}_clk$n \
