@@ -12,6 +12,7 @@
 #include "../../include/clipembed.h"
 #include "ce_kernels.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -907,8 +908,9 @@ size_t train_layout(const ce_handle* h, int B, TrainWs* w, char* base) {
     t.dpool = (float*)take((size_t)B * D * 4);
     t.du = (float*)take((size_t)B * E * 4);
     t.pooledT = (float*)take((size_t)B * D * 4);
-    t.colsum = (float*)take(std::max(ce::colsum_scratch_floats((int)M, (int)NX),
-                                     ce::act_bwd_colsum_scratch_floats((int)M, F)) * 4);
+    t.colsum = (float*)take(std::max({ce::colsum_scratch_floats((int)M, (int)NX), ce::act_bwd_colsum_scratch_floats((int)M, F),
+                                      ce::colsum_scratch_floats((int)M, 3 * (int)D),
+                                      ce::colsum_scratch_floats((int)B, 3 * (int)D)}) * 4);
     t.bpart = (float*)take((size_t)B * 3 * D * 4);      // attention backward: per-caption in_proj bias sums
     t.lnscr = (float*)take(ce::ln_bwd_scratch_floats((int)M, D) * 4);
     t.dres_b = (bf16_t*)take(M * D * 2);
@@ -1094,7 +1096,7 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         CE_TRY(tgemm(h, s, "dX_out", w.dres_b, D, w.WT, D, M, D, D, nullptr, 0, nullptr, w.dB, true, w.part));
         CE_TRY(timed(h, s, "attn_bwd", 10.0 * B * H * (double)L * L * 64, 0.0, [&] {
             return ce::launch_attention_bwd(w.dA, w.qkv[l], w.att[l], w.dB, w.lse[l], B, L, H, true, s,
-                                            G("attn.in_proj_bias"), w.bpart);
+                                            G("attn.in_proj_bias"), w.bpart, w.colsum);
         }));
         // in_proj: the engine's q rows carry kAttnQScale, so d(master q rows) = qs * d(engine q rows)
         CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_bias"), D, qs, s); }));

@@ -247,10 +247,11 @@ hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* d
 // dh == nullptr: out = act(pre); else out = dh * act'(pre).  bf16, n % 8 == 0.
 hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, int act, hipStream_t s);
 // attention backward (L <= 80): dqkv [B*L][3*H*64] from qkv (q pre-scaled), O, dO [B*L][H*64]
-// dbias (nullable): = column sums of dqkv over all rows (the in_proj bias gradient); bpart: [B][3*H*64] f32 scratch
+// dbias (nullable): = column sums of dqkv over all rows (the in_proj bias gradient); bpart: [B][3*H*64] f32 per-caption
+// sums; scratch: >= colsum_scratch_floats(max(B, B*L), 3*H*64) floats (both required with dbias)
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
                                 int B, int L, int H, bool causal, hipStream_t s, float* dbias = nullptr,
-                                float* bpart = nullptr);
+                                float* bpart = nullptr, float* scratch = nullptr);
 int set_attn_bwd_variant(int v);   // 2 = transposed-read kernel (default), 1 = the transposed-copy kernel
 // token / positional embedding gradients from dx [B*ctx][D] (dtok fully overwritten)
 size_t embed_bwd_scratch_bytes(int B, int ctx, int D);

@@ -117,10 +117,16 @@ __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, 
     __shared__ float red[4][64];
     const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
     const int n = blockIdx.x * 64 + c;
-    float a = 0.f;
-    if (n < N)
-        for (int b = r4; b < nb; b += 4) a += part[(size_t)b * N + n];
-    red[r4][c] = a;
+    // eight independent accumulators (eight loads in flight per lane), combined in a fixed order
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (n < N) {
+        int b = r4;
+        for (; b + 28 < nb; b += 32)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] += part[(size_t)(b + 4 * u) * N + n];
+        for (int u = 0; b < nb; b += 4, ++u) a[u] += part[(size_t)b * N + n];
+    }
+    red[r4][c] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
     if (r4 == 0 && n < N) {
         const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, 
 // dres_b (nullable): bf16 copy of the updated dres row (the next dX GEMM's operand); part_r (nullable):
 // per-block column sums of the updated dres (the bias gradient of the GEMM that produced the residual:
 // c_proj / out_proj, as the colsum of dres, fused)
-constexpr int LNB_ROWS = 16;   // rows per block (partial dw/db per block)
+constexpr int LNB_ROWS = 64;   // rows per block (partial dw/db per block)
 template <int NC>
 __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const float* __restrict__ x,
                                                 const float* __restrict__ dy, long ldy, const float* __restrict__ w,
@@ -887,8 +893,9 @@ hipError_t launch_act(bf16_t* out, const bf16_t* pre, const bf16_t* dh, long n, 
 constexpr size_t kAttnBwd2Lds = (size_t)(4 * AB_L * AB_LD + 2 * AB_L * AB2_LP) * 2 + (size_t)(2 * AB_L) * 4;
 constexpr size_t kAttnBwdLds = (size_t)(4 * AB_L * AB_LD + 3 * 64 * AB_LT + 3 * AB_L * AB_LT) * 2 + (size_t)(2 * AB_L) * 4;
 hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O, const bf16_t* dO, const float* lse,
-                                int B, int L, int H, bool causal, hipStream_t s, float* dbias, float* bpart) {
-    if (L <= 0 || L > AB_L || B <= 0 || !lse) return hipErrorInvalidValue;
+                                int B, int L, int H, bool causal, hipStream_t s, float* dbias, float* bpart,
+                                float* scratch) {
+    if (L <= 0 || L > AB_L || B <= 0 || !lse || (dbias && (!bpart || !scratch))) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
@@ -903,14 +910,13 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
         }
         hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse, L,
                            H, causal ? 1 : 0, dbias ? bpart : nullptr);
-        if (dbias)   // in_proj bias gradient: the captions' column sums, fixed order
-            hipLaunchKernelGGL(colsum_finish_k, dim3((unsigned)((3 * H * 64 + 63) / 64)), dim3(256), 0, s, dbias, bpart,
-                               B, 3 * H * 64, 1.0f, 0);
+        if (dbias)   // in_proj bias gradient: the captions' column sums (two-stage, fixed order)
+            return launch_colsum(dbias, bpart, true, 3 * H * 64, B, 3 * H * 64, 1.0f, false, scratch, s);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(attn_bwd_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwdLds, s, dqkv, qkv, O, dO, lse, L, H,
                        causal ? 1 : 0);
-    if (dbias) return launch_colsum(dbias, dqkv, false, 3 * H * 64, B * L, 3 * H * 64, 1.0f, false, bpart, s);
+    if (dbias) return launch_colsum(dbias, dqkv, false, 3 * H * 64, B * L, 3 * H * 64, 1.0f, false, scratch, s);
     return hipGetLastError();
 }
 

@@ -4,10 +4,12 @@ captions per GPU, so the text tower runs M = 1,536 x 77 = 118,272 rows through 1
 
 At that size the GEMM policy picks paths the toy-size test (tests/test_gpu_train.py, M = 462)
 never reaches: the four-wave persistent kernel for the forward QKV / c_fc GEMMs and every dX GEMM,
-and split-K + fixup for every weight-gradient GEMM (dW_*: grids of 9-36 tiles with K = 118,272).
-The test asserts those paths fired (ce_gemm_path_counts) and checks the step against
-  * the same step on the plain path (ce_set_gemm_auto(0) + ce_set_gemm_splitk(0): the 4-phase
-    kernel only, no split-K): loss and every gradient tensor, cosine >= 0.9999;
+and the MN-major weight-gradient GEMM (gemm_tn.hip: dW_* over K = 118,272 token rows, split-K over
+9-36 tiles) in place of transposed copies + the forward GEMM.  The test asserts those paths fired
+(ce_gemm_path_counts) and checks the step against
+  * the same step on the plain path (ce_set_gemm_auto(0) + ce_set_gemm_splitk(0) +
+    ce_set_train_dw_tn(0): the 4-phase kernel only, no split-K, dW on transposed copies): loss and
+    every gradient tensor, cosine >= 0.9999;
   * the reference's f32 autograd of the same step (oracle/text_train_torch.py, pinned to the
     reference's own training step in tests/test_oracle_train.py), run here in f32 on the GPU:
     every gradient tensor cosine >= 0.995 and norm within 3 %, loss within 5e-3 (the engine's
@@ -66,7 +68,7 @@ def c4():
     loss_big, g_big = run()
     cnt_big = path_counts()
     L = _lib.lib()
-    pa, ps = L.ce_set_gemm_auto(0), L.ce_set_gemm_splitk(0)
+    pa, ps, pt = L.ce_set_gemm_auto(0), L.ce_set_gemm_splitk(0), L.ce_set_train_dw_tn(0)
     try:
         path_counts()
         loss_plain, g_plain = run()
@@ -74,6 +76,7 @@ def c4():
     finally:
         L.ce_set_gemm_auto(pa)
         L.ce_set_gemm_splitk(ps)
+        L.ce_set_train_dw_tn(pt)
     return dict(m=m, tr=tr, img=img, caps=caps, loss_big=loss_big, g_big=g_big, cnt_big=cnt_big,
                 loss_plain=loss_plain, g_plain=g_plain, cnt_plain=cnt_plain)
 
@@ -88,15 +91,16 @@ def _views(tr, flat):
 
 
 def test_big_grid_paths_fire(c4):
-    """Per text block: QKV, c_fc and the four dX GEMMs on the four-wave persistent kernel; the four
-    dW GEMMs on the 4-phase kernel with split-K + fixup; out-proj / c_proj (residual epilogue) on
-    the 4-phase kernel.  The plain run uses neither the persistent kernel nor split-K."""
+    """Per text block: QKV, c_fc and the four dX GEMMs on the four-wave persistent kernel;
+    out-proj / c_proj (residual epilogue) on the 4-phase kernel; the four dW GEMMs on the MN-major
+    kernel (not counted by ce_gemm_path_counts).  The plain run uses neither the persistent kernel
+    nor split-K, and its dW GEMMs run on the 4-phase kernel over transposed copies."""
     nl = 12
     cnt = c4["cnt_big"]
     assert cnt[W4PP] == 6 * nl, cnt
-    assert cnt[FIXUP] == 4 * nl, cnt
-    assert cnt[NT] == 6 * nl, cnt
-    assert sum(cnt) == 16 * nl, cnt
+    assert cnt[FIXUP] == 0, cnt
+    assert cnt[NT] == 2 * nl, cnt
+    assert sum(cnt) == 8 * nl, cnt
     cp = c4["cnt_plain"]
     assert cp[W4PP] == 0 and cp[FIXUP] == 0 and cp[NT] == 12 * nl and sum(cp) == 12 * nl, cp
 
