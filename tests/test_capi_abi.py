@@ -70,5 +70,6 @@ def test_null_arguments_are_errors():
     assert L.ce_create(None, 0, None) == _lib.CE_ERR_INVALID
     assert L.ce_encode_image(None, None, None, 0, 1, 0, None, None, 0) == _lib.CE_ERR_INVALID
     assert L.ce_kernel_gemm_bf16(None, None, None, 1, 64, 64, None, 0, None, None, 0) == _lib.CE_ERR_INVALID
+    assert L.ce_kernel_gemm_tn_bf16(None, None, 256, None, 256, 256, 256, 64, None, 256, 0, 1.0) == _lib.CE_ERR_INVALID
     assert L.ce_set_ln_fold(None, 1, None) == _lib.CE_ERR_INVALID
     assert b"null" in L.ce_last_error()

@@ -49,7 +49,8 @@ def check(C, A, B, M, N, K, scale_rows=0, scale=1.0):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 1), (512, 256, 100), (768, 768, 462),
-                                   (768, 3072, 4096), (3072, 768, 9240), (2304, 768, 77 * 64)])
+                                   (768, 3072, 4096), (3072, 768, 9240), (2304, 768, 77 * 64),
+                                   (4096, 4096, 512)])
 def test_gemm_tn(M, N, K):
     g = torch.Generator(device="cpu").manual_seed(M + 3 * N + 7 * K)
     A = torch.randn(K, M, generator=g).to(torch.bfloat16).to(DEV)
@@ -66,6 +67,16 @@ def test_gemm_tn_strides_and_row_scale():
     C = run_tn(Aw, Bw, M, N, K, scale_rows=256, scale=0.18, ldc=N + 128)
     check(C, Aw, Bw, M, N, K, scale_rows=256, scale=0.18)
     assert torch.isnan(C[:, N:]).all()          # columns past N untouched
+
+
+def test_gemm_tn_one_chunk_direct_store():
+    """256 tiles = one workgroup per CU: no split, the kernel stores C itself and applies the row
+    scale there (scale_rows not a multiple of the tile)"""
+    M, N, K = 4096, 4096, 320
+    g = torch.Generator(device="cpu").manual_seed(9)
+    A = torch.randn(K, M, generator=g).to(torch.bfloat16).to(DEV)
+    B = torch.randn(K, N, generator=g).to(torch.bfloat16).to(DEV)
+    check(run_tn(A, B, M, N, K, scale_rows=1000, scale=0.5), A, B, M, N, K, scale_rows=1000, scale=0.5)
 
 
 def test_gemm_tn_full_size_deterministic():
