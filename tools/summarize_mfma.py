@@ -9,7 +9,8 @@ every SIMD's MFMA cycles: c_fc's 75.6 M v_mfma_f32_16x16x32_bf16 x 16 cycles = 1
 counted).  clock = GRBM_GUI_ACTIVE / 8 / duration.  `frac_at_nominal` = mfma_busy x clock / 2.4 GHz,
 comparable with bench.py's event-timed FLOP fraction of the 2.5 PF/s (2.4 GHz) peak.
 Kernel classes map to the engine's tags by name, grid and duration (out-proj and c_proj share the
-staged-residual kernel and grid; c_proj's K = 4096 launches run ~2x longer)."""
+staged-residual kernel and grid; c_proj's K = 4096 launches run ~2x longer; the thresholds are the
+B = 256 inference bench's, so over a NegCLIP run only dW_tn and attn_v are clean classes)."""
 import argparse
 import collections
 import csv
@@ -19,6 +20,8 @@ import re
 
 
 def tag_of(name, grid, ms):
+    if "gemm_tn_w4" in name:
+        return "dW_tn"
     if "gemm_w4_resid_hl" in name and grid == 65536:
         return "gemm_proj_v" if ms > 0.6 else "gemm_out_v"
     if "gemm_bf16_w4pp<1" in name and grid == 65536:
