@@ -163,6 +163,8 @@ class TextTowerTrainer:
         _lib.call("ce_train_bind", self.e.h, P, G, len(order))
         _lib.call("ce_train_sync_weights", self.e.h, _stream(self.dev))
         self.lossbuf = torch.zeros(2, device=self.dev, dtype=torch.float32)
+        self.overlap_text = True            # text forward beside the image forward (compute_grads)
+        self._side = None
 
     # ------------------------------------------------------------------ pieces
     @property
@@ -188,13 +190,34 @@ class TextTowerTrainer:
     # ------------------------------------------------------------------ the step
     def compute_grads(self, images: torch.Tensor, texts: torch.Tensor) -> torch.Tensor:
         """Steps 1-5: forward, ClipLoss, backward, gradient all-reduce.  Returns the local loss (device
-        scalar, no host sync); gradients are in self.grad / self.gviews."""
+        scalar, no host sync); gradients are in self.grad / self.gviews.
+
+        The locked image tower and the text tower's forward are independent until the loss, so with
+        `overlap_text` (default) the text forward runs on a side stream beside the image forward
+        (its kernels take the CUs the image tower's launches leave idle); the loss waits for both."""
+        if not self.overlap_text:
+            img = self.model.encode_image(images, normalize=True)
+            return self.compute_grads_from_features(img, texts)
+        main = torch.cuda.current_stream(self.dev)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        side = self._side
+        texts = texts.to(self.dev, torch.int64).contiguous()
+        side.wait_stream(main)                      # the caption ids (and the weights) are ready
+        with torch.cuda.stream(side):
+            txt = self.text_forward(texts)
+        texts.record_stream(side)
         img = self.model.encode_image(images, normalize=True)
-        return self.compute_grads_from_features(img, texts)
+        main.wait_stream(side)
+        txt.record_stream(main)
+        return self._grads_from_text(img, txt)
 
     def compute_grads_from_features(self, img: torch.Tensor, texts: torch.Tensor) -> torch.Tensor:
         """Steps 2-5 given the locked image tower's normalised features img [B, E] (step 1)."""
-        txt = self.text_forward(texts)
+        return self._grads_from_text(img, self.text_forward(texts))
+
+    def _grads_from_text(self, img: torch.Tensor, txt: torch.Tensor) -> torch.Tensor:
+        """Steps 3-5 given both towers' features (txt from ce_text_forward_train on this handle)."""
         scale = math.exp(float(self.logit_scale))
         dtxt = self.loss_and_feature_grad(img, txt, scale)
         _lib.call("ce_text_backward", self.e.h, _stream(self.dev), _ptr(dtxt), txt.shape[0])

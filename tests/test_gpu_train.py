@@ -98,3 +98,24 @@ def test_bind_errors():
     tr = TextTowerTrainer(m)
     with pytest.raises(ClipEmbedError, match="batch"):
         _lib.call("ce_text_backward", m.engine.h, _stream(m.engine.device), _ptr(d), 2)
+
+
+def test_text_forward_overlap_is_bitwise_neutral(golden):
+    """compute_grads runs the text forward on a side stream beside the locked image forward; the
+    gradients and loss must equal the serial order's bit for bit (same kernels, same inputs)."""
+    g = golden("train")
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 2)
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(W.synthetic_state_dict(cfg))
+    m.to("cuda")
+    tr = TextTowerTrainer(m, lr=LR, weight_decay=WD, usehardtext=True)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=int(g["images_seed"]))).cuda()
+    caps = torch.from_numpy(g["captions"]).cuda()
+    out = {}
+    for overlap in (False, True):
+        tr.overlap_text = overlap
+        loss = tr.compute_grads(imgs, caps)
+        torch.cuda.synchronize()
+        out[overlap] = (float(loss), tr.grad.clone())
+    assert out[True][0] == out[False][0]
+    assert torch.equal(out[True][1], out[False][1])
