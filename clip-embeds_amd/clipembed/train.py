@@ -163,7 +163,7 @@ class TextTowerTrainer:
         _lib.call("ce_train_bind", self.e.h, P, G, len(order))
         _lib.call("ce_train_sync_weights", self.e.h, _stream(self.dev))
         self.lossbuf = torch.zeros(2, device=self.dev, dtype=torch.float32)
-        self.overlap_text = True            # text forward beside the image forward (compute_grads)
+        self.overlap_text = False           # text forward beside the image forward (compute_grads)
         self._side = None
 
     # ------------------------------------------------------------------ pieces
@@ -192,9 +192,11 @@ class TextTowerTrainer:
         """Steps 1-5: forward, ClipLoss, backward, gradient all-reduce.  Returns the local loss (device
         scalar, no host sync); gradients are in self.grad / self.gviews.
 
-        The locked image tower and the text tower's forward are independent until the loss, so with
-        `overlap_text` (default) the text forward runs on a side stream beside the image forward
-        (its kernels take the CUs the image tower's launches leave idle); the loss waits for both."""
+        The locked image tower and the text tower's forward are independent until the loss: with
+        `overlap_text` the text forward runs on a side stream beside the image forward and the loss
+        waits for both.  Off by default: at the C4 size both towers' GEMMs are persistent grids of
+        one workgroup per CU, so they take turns rather than fill each other's gaps (NegCLIP 453.7 vs
+        451.8 ms/step)."""
         if not self.overlap_text:
             img = self.model.encode_image(images, normalize=True)
             return self.compute_grads_from_features(img, texts)
