@@ -63,7 +63,7 @@ def main():
     # name: (N, K, act, epi, resid, out_bf16)
     shapes = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True, False),
               "fc": (4096, 1024, 1, 2, False, True), "proj": (1024, 4096, 0, 1, True, False),
-              "fc_plain": (4096, 1024, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True), "sq": (4096, 4096, 0, 0, False, True),
+              "fc_plain": (4096, 1024, 0, 0, False, True), "proj_plain": (1024, 4096, 0, 0, False, True), "fc_fold": (4096, 1024, 0, 2, False, True), "sq": (4096, 4096, 0, 0, False, True),
               # hi/lo residual stream (epi 3: resid and xb are [2][M][N] bf16 planes, no f32 output)
               "out_hl": (1024, 1024, 0, 3, True, False), "proj_hl": (1024, 4096, 0, 3, True, False)}
     if args.only:
