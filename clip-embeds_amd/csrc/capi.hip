@@ -1049,8 +1049,10 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
                                           grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
                                           w.lnscr, s, w.dres_b, grad_of(h, top + "mlp.c_proj.bias")); }));
     const float qs = ce::kAttnQScale;
-    // MN-major dW GEMMs: widths that are multiples of 256 (ViT-B/L text towers: 512, 768)
-    const bool tn = dw_tn() && D % 256 == 0 && F % 256 == 0;
+    // MN-major dW GEMMs: widths that are multiples of 256 (ViT-B/L text towers: 512, 768) and
+    // activations under the kernel's 32-bit DMA offsets (< 2 GB: up to ~340k token rows at F = 3072);
+    // otherwise the transposed copies
+    const bool tn = dw_tn() && D % 256 == 0 && F % 256 == 0 && (long)M * std::max(3 * D, F) * 2 <= 0x7fe00000L;
     for (int l = w.nl - 1; l >= 0; --l) {
         const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
         const Blk k = block_ptrs(h, pfx);
