@@ -1053,6 +1053,7 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
     // activations under the kernel's 32-bit DMA offsets (< 2 GB: up to ~340k token rows at F = 3072);
     // otherwise the transposed copies
     const bool tn = dw_tn() && D % 256 == 0 && F % 256 == 0 && (long)M * std::max(3 * D, F) * 2 <= 0x7fe00000L;
+    bf16_t* const dxb = reinterpret_cast<bf16_t*>(w.dxn);     // [M][D] bf16 in the f32 buffer's space
     for (int l = w.nl - 1; l >= 0; --l) {
         const std::string pfx = "transformer.resblocks." + std::to_string(l) + ".";
         const Blk k = block_ptrs(h, pfx);
@@ -1081,10 +1082,12 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
                          w.part));
         }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, F, k.wfc, false, D, F, D, F, s); }));
-        CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, w.dxn, false, w.part));
-        CE_TRY(timed(h, s, "t_ln_2_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.XM[l], w.dxn, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
+        // (the LN-input gradients in bf16, as autocast's matmul gradients: half the bytes out of the dX
+        // GEMMs and into the LN backward)
+        CE_TRY(tgemm(h, s, "dX_fc", w.dA, F, w.WT, F, M, D, F, nullptr, 0, nullptr, dxb, true, w.part));
+        CE_TRY(timed(h, s, "t_ln_2_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.XM[l], nullptr, D, k.ln2w, nullptr, M, D, G("ln_2.weight"),
                                               G("ln_2.bias"), true, false, w.lnscr, s, w.dres_b,
-                                              G("attn.out_proj.bias")); }));
+                                              G("attn.out_proj.bias"), dxb); }));
         // ---- attention: XM = X + out_proj(MHA(ln_1 X))  (transformer.py:242-255, 266) ----
         if (tn) {
             CE_TRY(tgemm_tn(h, s, "dW_out", w.dres_b, D, w.att[l], D, D, D, M, G("attn.out_proj.weight"), w.part));
@@ -1113,12 +1116,12 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
             CE_TRY(timed(h, s, "t_scale", 0.0, 0.0, [&] { return ce::launch_scale(G("attn.in_proj_weight"), (long)D * D, qs, s); }));
         }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, 3 * D, k.wqkv, false, D, 3 * D, D, 3 * D, s); }));
-        CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, w.dxn, false, w.part));
+        CE_TRY(tgemm(h, s, "dX_qkv", w.dA, 3 * D, w.WT, 3 * D, M, D, 3 * D, nullptr, 0, nullptr, dxb, true, w.part));
         // (dres is now the gradient of X[l] = the c_proj output of block l - 1: its bf16 copy and that
         // bias's column sums come out of this kernel)
         float* below = l > 0 ? grad_of(h, "transformer.resblocks." + std::to_string(l - 1) + ".mlp.c_proj.bias") : nullptr;
-        CE_TRY(timed(h, s, "t_ln_1_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[l], w.dxn, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
-                                              G("ln_1.bias"), true, false, w.lnscr, s, w.dres_b, below); }));
+        CE_TRY(timed(h, s, "t_ln_1_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[l], nullptr, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
+                                              G("ln_1.bias"), true, false, w.lnscr, s, w.dres_b, below, dxb); }));
     }
     // token / positional embeddings (model.py:286-288)
     CE_TRY(timed(h, s, "t_embed_bwd", 0.0, 0.0, [&] { return ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),

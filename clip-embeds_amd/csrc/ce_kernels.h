@@ -239,7 +239,8 @@ hipError_t launch_colsum(float* out, const void* in, bool in_f32, long ld, int M
 long ln_bwd_scratch_floats(int n, int D);
 hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
                          int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
-                         hipStream_t s, bf16_t* dres_b = nullptr, float* dsum = nullptr);
+                         hipStream_t s, bf16_t* dres_b = nullptr, float* dsum = nullptr,
+                         const bf16_t* dy_b = nullptr);   // dy_b: bf16 dy (row stride ldy) in place of dy
 // out = dh * act'(pre) over [M][N] bf16 and dbias = column sums of out (scratch >= act_bwd_colsum_scratch_floats)
 long act_bwd_colsum_scratch_floats(int M, int N);
 hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* dh, int M, int N, int act, float* dbias,

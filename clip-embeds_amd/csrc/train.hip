@@ -143,9 +143,10 @@ __global__ __launch_bounds__(256) void colsum_finish_k(float* __restrict__ out, 
 // per-block column sums of the updated dres (the bias gradient of the GEMM that produced the residual:
 // c_proj / out_proj, as the colsum of dres, fused)
 constexpr int LNB_ROWS = 64;   // rows per block (partial dw/db per block)
-template <int NC>
+// DYB: dy is bf16 (the dX GEMMs' output, as autocast's bf16 matmul gradients), read 8 B per 4 values
+template <int NC, bool DYB>
 __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const float* __restrict__ x,
-                                                const float* __restrict__ dy, long ldy, const float* __restrict__ w,
+                                                const void* __restrict__ dyv, long ldy, const float* __restrict__ w,
                                                 const int* __restrict__ rows, int n, float* __restrict__ part_w,
                                                 float* __restrict__ part_b, int accumulate, bf16_t* __restrict__ dres_b,
                                                 float* __restrict__ part_r) {
@@ -164,7 +165,13 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const 
         for (int c = 0; c < NC; ++c) {
             const int e = c * 256 + lane * 4;
             v[c] = *reinterpret_cast<const float4*>(x + xr * D + e);
-            d[c] = *reinterpret_cast<const float4*>(dy + (long)i * ldy + e);
+            if constexpr (DYB) {
+                const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(dyv) + (long)i * ldy + e);
+                d[c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                   __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+            } else {
+                d[c] = *reinterpret_cast<const float4*>(static_cast<const float*>(dyv) + (long)i * ldy + e);
+            }
             s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
         }
         const float mean = wave_sum(s) / (float)D;
@@ -856,18 +863,21 @@ long ln_bwd_scratch_floats(int n, int D) {
 }
 hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy, const float* w, const int* rows, int n,
                          int D, float* dw, float* db, bool accumulate_dx, bool accumulate_dwb, float* scratch,
-                         hipStream_t s, bf16_t* dres_b, float* dsum) {
+                         hipStream_t s, bf16_t* dres_b, float* dsum, const bf16_t* dy_b) {
     if (n <= 0) return hipSuccess;
     const int nb = (n + LNB_ROWS - 1) / LNB_ROWS;
     float* pw = scratch;
     float* pb = scratch + (size_t)nb * D;
     float* pr = dsum ? pb + (size_t)nb * D : nullptr;
     const int acc = accumulate_dx ? 1 : 0;
-#define CE_LNB(NC) hipLaunchKernelGGL(ln_bwd_k<NC>, dim3(nb), dim3(256), 0, s, dres, x, dy, ldy, w, rows, n, pw, pb, acc, \
-                                      dres_b, pr)
-    if (D == 768) CE_LNB(3);
-    else if (D == 1024) CE_LNB(4);
-    else if (D == 512) CE_LNB(2);
+#define CE_LNB(NC) \
+    if (dy_b) hipLaunchKernelGGL((ln_bwd_k<NC, true>), dim3(nb), dim3(256), 0, s, dres, x, (const void*)dy_b, ldy, w, rows, n, \
+                                 pw, pb, acc, dres_b, pr); \
+    else hipLaunchKernelGGL((ln_bwd_k<NC, false>), dim3(nb), dim3(256), 0, s, dres, x, (const void*)dy, ldy, w, rows, n, pw, \
+                            pb, acc, dres_b, pr)
+    if (D == 768) { CE_LNB(3); }
+    else if (D == 1024) { CE_LNB(4); }
+    else if (D == 512) { CE_LNB(2); }
     else return hipErrorInvalidValue;
 #undef CE_LNB
     float* cscr = pb + 2 * (size_t)nb * D;
