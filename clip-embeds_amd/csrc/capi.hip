@@ -1005,9 +1005,16 @@ int run_text_train(ce_handle* h, hipStream_t s, TrainWs& w, const int64_t* ids) 
         CE_TRY(tgemm(h, s, "train_out", w.att[l], D, k.wout, D, M, D, D, k.bout, ce::ACT_NONE_, w.X[l], w.XM[l], false,
                      w.part));
         CE_TRY(layernorm(h, s, "ln_t", w.XM[l], w.xn2[l], true, k.ln2w, k.ln2b, M, D));
-        CE_TRY(tgemm(h, s, "train_fc", w.xn2[l], D, k.wfc, D, M, F, D, k.bfc, ce::ACT_NONE_, nullptr, w.pre[l], true,
-                     w.part));
-        CE_TRY(timed(h, s, "t_act", 0.0, 0.0, [&] { return ce::launch_act(w.hh[l], w.pre[l], nullptr, (long)M * F, act_code(h), s); }));
+        {   // c_fc: the activation and the pre-activation copy the backward needs from one epilogue
+            ce::GemmParams p{};
+            p.A = w.xn2[l]; p.lda = D; p.W = k.wfc; p.ldw = D;
+            p.M = M; p.N = F; p.K = D;
+            p.bias = k.bfc;
+            p.out = w.hh[l]; p.ldo = F;
+            p.pre_out = w.pre[l];
+            p.part = w.part; p.part_elems = ce::kGemmPartElems;
+            CE_TRY(timed(h, s, "train_fc", 2.0 * M * F * D, 0.0, [&] { return ce::launch_gemm(p, act_code(h), true, s); }));
+        }
         CE_TRY(tgemm(h, s, "train_proj", w.hh[l], F, k.wproj, F, M, D, F, k.bproj, ce::ACT_NONE_, w.XM[l], w.X[l + 1],
                      false, w.part));
     }

@@ -56,6 +56,9 @@ struct GemmParams {
     // packed rows (the text tower's pooled-only calls): only the first *m_dev of the M rows are live;
     // tiles past them exit.  Implies one tile per workgroup and no split-K tail (launch_gemm).
     const int* m_dev = nullptr;
+    // bf16 output with an activation (EPI_PLAIN, no residual): also store the pre-activation values
+    // (bias added) here, same layout as out (the training forward keeps both for the backward)
+    bf16_t* pre_out = nullptr;
 };
 // EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)

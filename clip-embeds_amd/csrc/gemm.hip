@@ -439,11 +439,17 @@ __device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f3
 #pragma unroll
         for (int i = 0; i < 8; ++i) st[i] = ss[16 * i];
     }
+    // pre-activation copy (training forward, EPI_PLAIN only: the inference epilogues keep their code)
+    constexpr bool MAYPRE = EPI == EPI_PLAIN && ACT != ACT_NONE;
+    const bool pre = MAYPRE && p.pre_out != nullptr;            // wave-uniform
+    __amdgpu_buffer_rsrc_t psrd = osrd;
+    if constexpr (MAYPRE)
+        if (pre) psrd = make_srd(p.pre_out + (size_t)mbase * p.ldo, rows * (int)p.ldo * 2);
 #pragma unroll
     for (int ip = 0; ip < 4; ++ip) {
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
-            uint2 h[2];
+            uint2 h[2], hp[2];
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 f32x4 v = acc[2 * ip + r][j];
@@ -458,6 +464,8 @@ __device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f3
                 } else {
                     v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
                 }
+                if constexpr (MAYPRE)
+                    if (pre) hp[r] = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
                 if constexpr (ACT == ACT_GELU) {
                     v = gelu_fast4(v);
                 } else {
@@ -470,6 +478,14 @@ __device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f3
             const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
             const u32x4 d = {x[0], y[0], x[1], y[1]};
             __builtin_amdgcn_raw_buffer_store_b128(d, osrd, voff + j * 32, 0, 0);
+            if constexpr (MAYPRE) {
+                if (pre) {
+                    const auto px = __builtin_amdgcn_permlane16_swap(hp[0].x, hp[1].x, false, false);
+                    const auto py = __builtin_amdgcn_permlane16_swap(hp[0].y, hp[1].y, false, false);
+                    const u32x4 dp = {px[0], py[0], px[1], py[1]};
+                    __builtin_amdgcn_raw_buffer_store_b128(dp, psrd, voff + j * 32, 0, 0);
+                }
+            }
         }
         voff += 32 * ldo2;
     }
@@ -2899,6 +2915,23 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     }
     if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
+    if (p.pre_out) {
+        // pre-activation copy: written by the four-wave kernel's one-wave-per-SIMD epilogue (the
+        // default policy's path for this GEMM); on any other path the GEMM writes pre and the
+        // activation kernel forms out = act(pre)
+        if (act == ACT_NONE || !out_bf16 || res || epi != EPI_PLAIN || p.grp || p.m_dev || p.ldo != p.N)
+            return hipErrorInvalidValue;
+        const bool fused = !p.onetile && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
+                           !(p.variant & GEMM_VAR_W4_TAIL);
+        if (!fused) {
+            GemmParams q = p0;
+            q.out = p.pre_out;
+            q.pre_out = nullptr;
+            const hipError_t e = launch_gemm(q, ACT_NONE, true, s, epi);
+            if (e != hipSuccess) return e;
+            return launch_act(static_cast<bf16_t*>(p.out), p.pre_out, nullptr, (long)p.M * p.N, act, s);
+        }
+    }
     if (p.rhl && epi != EPI_LN_STATS_HL && epi != EPI_HL_F32) return hipErrorInvalidValue;
     if (epi == EPI_LN_STATS) {
         if (act != ACT_NONE || !res || out_bf16 || !p.xb || !p.stats_part) return hipErrorInvalidValue;
