@@ -581,30 +581,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv,
         else if (which == 1) r = mfma_tile2<true, true>(dSs, AB2_LP, Qs, AB_LD, m0, n0, K, lane);
         else r = mfma_tile2<true, true>(Ps, AB2_LP, dOs, AB_LD, m0, n0, K, lane);
         const int col = which * D + h * 64 + n0 + (lane & 15);
-        // bf16 values of rows m0 + 4 (lane >> 4) + q; adjacent columns sit in lanes l, l ^ 1, so an even
-        // lane stores the (col, col + 1) pair of rows q = 0, 2 and an odd lane that of rows 1, 3: two
-        // 4-B stores per lane instead of four 2-B ones
-        bf16_t vb[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) vb[q] = f2bf(r[q]);
-        const uint32_t mine01 = (uint32_t)vb[0] | ((uint32_t)vb[1] << 16);
-        const uint32_t mine23 = (uint32_t)vb[2] | ((uint32_t)vb[3] << 16);
-        const uint32_t oth01 = (uint32_t)__shfl_xor((int)mine01, 1, 64);
-        const uint32_t oth23 = (uint32_t)__shfl_xor((int)mine23, 1, 64);
-        const bool odd = (lane & 1) != 0;
-        const int ib = m0 + 4 * (lane >> 4);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int q = 2 * k + (odd ? 1 : 0);
-            const uint32_t mv = k ? mine23 : mine01, ov = k ? oth23 : oth01;
-            const uint32_t self = odd ? (mv >> 16) : (mv & 0xffffu), part = odd ? (ov >> 16) : (ov & 0xffffu);
-            const uint32_t pair = odd ? (part | (self << 16)) : (self | (part << 16));
-            if (ib + q < L)
-                *reinterpret_cast<uint32_t*>(dqkv + (size_t)(b * L + ib + q) * ld + col - (odd ? 1 : 0)) = pair;
+        for (int q = 0; q < 4; ++q) {
+            const int i = m0 + 4 * (lane >> 4) + q;
+            if (i < L) {
+                const bf16_t v = f2bf(r[q]);
+                dqkv[(size_t)(b * L + i) * ld + col] = v;
+                csum += bf2f(v);
+            }
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (ib + q < L) csum += bf2f(vb[q]);
         if (bpart && (tt >> 2) == nt - 1) {       // last row tile of this column block: reduce, store
             csum += __shfl_xor(csum, 16, 64);
             csum += __shfl_xor(csum, 32, 64);
