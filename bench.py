@@ -344,6 +344,27 @@ def build_sparc(args, dev, rank, world):
 BUILDERS = {"clip": build_clip, "pacl": build_pacl, "negclip": build_negclip, "sparc": build_sparc}
 
 
+def gloo_device_reduce_scatter():
+    """Rehearsal backend only (--dist-backend gloo): some torch builds' gloo has no reduce_scatter for
+    device tensors; the NegCLIP trainer's one reduce_scatter_tensor is then staged through host memory
+    in this process.  The RCCL path (the default backend) never takes this."""
+    try:
+        o = torch.zeros(2, device="cuda")
+        dist.reduce_scatter_tensor(o, torch.ones(2 * dist.get_world_size(), device="cuda"))
+        return False
+    except (RuntimeError, ValueError, NotImplementedError):
+        real = dist.reduce_scatter_tensor
+
+        def host_staged(output, input, op=dist.ReduceOp.SUM, group=None, async_op=False):
+            o = output.cpu()
+            real(o, input.cpu(), op=op, group=group)
+            output.copy_(o)
+
+        dist.reduce_scatter_tensor = host_staged
+        log("gloo: reduce_scatter of device tensors staged through host memory (rehearsal backend)")
+        return True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -394,6 +415,7 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
+            gloo_device_reduce_scatter()
 
     if args.attn_var >= 0:
         from clipembed import _lib

@@ -25,6 +25,7 @@
 
 #include "ce_device.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 namespace ce {
 namespace {
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     }
 }
 
-int g_attn_var = 381;
+std::atomic<int> g_attn_var{381};     // A/B knob (knobs.h: process-wide atomic)
 
 // One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
 // mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
@@ -712,7 +713,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
 #define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
-    const int v = g_attn_var;
+    const int v = g_attn_var.load(std::memory_order_acquire);
     if (causal) {
         if ((v & 88) == 88) CE_ATTN_LAUNCH(true, 88);
         else if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
@@ -742,7 +743,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 }
 
 int set_attn_variant(int var) {
-    const int prev = g_attn_var;
+    const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381)
                      ? var : 381;

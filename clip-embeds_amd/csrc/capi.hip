@@ -11,6 +11,7 @@
 // weights and accumulates in f32 (MFMA); LayerNorm statistics are f32.
 #include "../../include/clipembed.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <cmath>
@@ -967,14 +968,9 @@ int tgemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long ld
 }
 
 // weight gradients by the MN-major GEMM (gemm_tn.hip) or, 0, by transposed copies + the forward GEMM
-int g_dw_tn = -1;
-bool dw_tn() {
-    if (g_dw_tn < 0) {
-        const char* e = std::getenv("CE_TRAIN_DW_TN");
-        g_dw_tn = e ? (std::atoi(e) != 0) : 1;
-    }
-    return g_dw_tn != 0;
-}
+std::atomic<int> g_dw_tn{ce::kKnobUnset};     // A/B knob (knobs.h)
+int dw_tn_env() { return ce::env_int("CE_TRAIN_DW_TN", 1) != 0; }
+bool dw_tn() { return ce::knob_get(g_dw_tn, dw_tn_env) != 0; }
 
 // dW[M][N] = scale_m * sum over the T token rows of A[t][m] B[t][n]  (row-major activations in place)
 int tgemm_tn(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M,
@@ -2180,7 +2176,7 @@ int ce_set_gemm_schedule(int schedule) { return ce::set_gemm_schedule(schedule);
 int ce_set_attn_bwd_variant(int v) { return ce::set_attn_bwd_variant(v); }
 int ce_set_train_dw_tn(int on) {
     const int prev = dw_tn() ? 1 : 0;
-    g_dw_tn = on ? 1 : 0;
+    g_dw_tn.store(on ? 1 : 0);
     return prev;
 }
 int ce_kernel_gemm_tn_bf16(void* stream, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,

@@ -59,6 +59,11 @@ struct GemmParams {
     // bf16 output with an activation (EPI_PLAIN, no residual): also store the pre-activation values
     // (bias added) here, same layout as out (the training forward keeps both for the backward)
     bf16_t* pre_out = nullptr;
+    // the process-wide schedule knobs (knobs.h), read once by launch_gemm so one launch never mixes
+    // values another thread sets meanwhile
+    struct {
+        int sched = 1, autom = 1, splitk = 1, groupm = 4, stagger = 0, ring = 4;
+    } kn;
 };
 // EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)

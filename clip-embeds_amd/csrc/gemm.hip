@@ -21,12 +21,14 @@
 //    A row-panel land on the same XCD and share its L2.
 #include "ce_device.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <type_traits>
 #include <utility>
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
 
 #ifndef CE_RESID_RING
 #define CE_RESID_RING 4
@@ -2424,79 +2426,45 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_w2(GemmParams p) {
     trace_stamp(p, 2);
 }
 
-int g_variant = -1;
-int gemm_variant() {
-    if (g_variant < 0) {
-        const char* e = getenv("CE_GEMM_VARIANT");
-        g_variant = e ? std::max(0, atoi(e)) : CE_GEMM_VAR_DEFAULT;
-    }
-    return g_variant;
-}
+// Process-wide A/B knobs (knobs.h: atomics, env value published by the first reader)
+std::atomic<int> g_variant{kKnobUnset};
+int variant_env() { const int v = env_int("CE_GEMM_VARIANT", CE_GEMM_VAR_DEFAULT); return v < 0 ? 0 : v; }
+int gemm_variant() { return knob_get(g_variant, variant_env); }
 
-int g_sched = -1;
-int g_ring = CE_RESID_RING;     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
-unsigned long long* g_trace = nullptr;
-long g_trace_n = 0;
-int g_stagger = -1;             // first-round de-synchronisation sleep (units of s_sleep 127)
-int gemm_stagger() {
-    if (g_stagger < 0) {
-        const char* e = getenv("CE_GEMM_STAGGER");
-        g_stagger = e ? std::max(0, atoi(e)) : 0;
-    }
-    return g_stagger;
+bool sched_ok(int sc) {
+    return sc == 0 || sc == 1 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 ||
+           sc == 11 || sc == 12 || sc == 13;
 }
-int gemm_sched() {
-    if (g_sched < 0) {
-        const char* e = getenv("CE_GEMM_SCHED");
-        g_sched = e ? atoi(e) : 1;
-        if (!(g_sched == 0 || g_sched == 1 || g_sched == 2 || g_sched == 3 || g_sched == 4 || g_sched == 6 ||
-              g_sched == 7 || g_sched == 9 || g_sched == 10 || g_sched == 11 || g_sched == 12 || g_sched == 13))
-            g_sched = 1;
-    }
-    return g_sched;
-}
+std::atomic<int> g_sched{kKnobUnset};
+std::atomic<int> g_ring{CE_RESID_RING};     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
+// diagnostic timeline buffer (ce_set_gemm_trace): process-wide by contract (clipembed.h)
+std::atomic<unsigned long long*> g_trace{nullptr};
+std::atomic<long> g_trace_n{0};
+std::atomic<int> g_stagger{kKnobUnset};     // first-round de-synchronisation sleep (units of s_sleep 127)
+int stagger_env() { return std::max(0, env_int("CE_GEMM_STAGGER", 0)); }
+int gemm_stagger() { return knob_get(g_stagger, stagger_env); }
+int sched_env() { const int s = env_int("CE_GEMM_SCHED", 1); return sched_ok(s) ? s : 1; }
+int gemm_sched() { return knob_get(g_sched, sched_env); }
 
-int g_num_cu = 0;
-int num_cus() {
-    if (g_num_cu <= 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            g_num_cu = n;
-        else
-            g_num_cu = 256;
-    }
-    return g_num_cu;
-}
+int num_cus() { return device_cus(); }
 
-int g_groupm = -1;
-int gemm_groupm() {
-    if (g_groupm < 0) {
-        const char* e = getenv("CE_GEMM_GROUPM");
-        g_groupm = e ? atoi(e) : 4;
-        if (g_groupm < 1 || g_groupm > 64) g_groupm = 1;
-    }
-    return g_groupm;
-}
+std::atomic<int> g_groupm{kKnobUnset};
+int groupm_env() { const int g = env_int("CE_GEMM_GROUPM", 4); return (g < 1 || g > 64) ? 1 : g; }
+int gemm_groupm() { return knob_get(g_groupm, groupm_env); }
 
 // Split-K tail plan: with one 512-thread workgroup per CU, a grid of T tiles runs in ceil(T / CUs)
 // rounds; when the last round holds only R = T % CUs tiles (vision out-proj / c_proj at B = 256:
 // 2308 tiles = 9 rounds + 4 tiles) the chip idles for most of a tile time.  Those R tiles are split
 // into S K-chunks (R * S <= CUs) so the last round is ~1/S of a tile, plus a tiny fixup launch.
-int g_splitk = -1;
-bool splitk_enabled() {
-    if (g_splitk < 0) {
-        const char* e = getenv("CE_GEMM_SPLITK");
-        g_splitk = e ? (atoi(e) != 0) : 1;
-    }
-    return g_splitk != 0;
-}
+std::atomic<int> g_splitk{kKnobUnset};
+int splitk_env() { return env_int("CE_GEMM_SPLITK", 1) != 0; }
+bool splitk_enabled() { return knob_get(g_splitk, splitk_env) != 0; }
 
 void plan_tail(GemmParams& p, int nwg) {
     p.tail = 0;
     p.split = 1;
     const int C = num_cus(), nk = p.K / BK;
-    if (!splitk_enabled() || !p.part) return;
+    if (!p.kn.splitk || !p.part) return;
     int R, cap;
     if ((nwg <= C / 2 && nk >= 32) || (nwg <= C / 16 && nk >= 8)) {
         // small grid, long K (weight gradients: M = out features, K = tokens), or a grid of a few
@@ -2517,11 +2485,16 @@ void plan_tail(GemmParams& p, int nwg) {
 }
 
 // Per-device partial-tile workspace for the kernel-level entry point (engine handles pass their own).
-float* g_part[64] = {};
+// Allocated once per device under a lock (kernel-level callers on several threads); the slabs are
+// used by one launch at a time per device stream order — concurrent kernel-level GEMMs with a
+// split-K tail on two streams of one device would share them, so the engine passes its own.
+float* g_part[kMaxDevices] = {};
+std::mutex g_part_mu;
 constexpr long kPartElems = 256L * BM * BN;     // 64 MB: R * S <= 256 slabs
 float* kernel_api_part() {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_part_mu);
     if (!g_part[dev] && hipMalloc(&g_part[dev], kPartElems * sizeof(float)) != hipSuccess) {
         (void)hipGetLastError();
         g_part[dev] = nullptr;
@@ -2545,7 +2518,7 @@ bool w4_epi2(const GemmParams& p) {
 void plan_tail_w4(GemmParams& p, int nwg, int grid) {
     p.tail = 0;
     p.split = 1;
-    if (!splitk_enabled() || !p.part || !(gemm_variant() & GEMM_VAR_W4_TAIL)) return;
+    if (!p.kn.splitk || !p.part || !(p.variant & GEMM_VAR_W4_TAIL)) return;
     const int r = nwg % grid, nk = p.K / BK;
     if (nwg < grid || r == 0 || r > grid / 8) return;
     int S = std::min(std::min(std::max(nk / 4, 2), 16), std::min(grid / r, nk));
@@ -2561,7 +2534,7 @@ void plan_tail_w4(GemmParams& p, int nwg, int grid) {
 void plan_tail_rhl(GemmParams& p, int nwg, int grid) {
     p.tail = 0;
     p.split = 1;
-    if (!splitk_enabled() || !p.part) return;
+    if (!p.kn.splitk || !p.part) return;
     const int r = nwg % grid, nk = p.K / BK;
     if (nwg < grid || r == 0 || r > grid / 8) return;
     int S = std::min(std::min(std::max(nk / 4, 2), 16), std::min(grid / r, nk));
@@ -2573,9 +2546,9 @@ void plan_tail_rhl(GemmParams& p, int nwg, int grid) {
 
 // SCHED 11 grid: one workgroup per CU, a multiple of 8 so every XCD group is complete
 // (GEMM_VAR_W4_ONETILE: one workgroup per tile)
-int w4pp_grid(int nwg, bool onetile = false) {
+int w4pp_grid(const GemmParams& p, int nwg, bool onetile = false) {
     const int need = ((nwg + 7) / 8) * 8;
-    if (onetile || (gemm_variant() & GEMM_VAR_W4_ONETILE)) return need;
+    if (onetile || (p.variant & GEMM_VAR_W4_ONETILE)) return need;
     const int grid = (num_cus() / 8) * 8;
     return grid < need ? grid : need;
 }
@@ -2588,19 +2561,13 @@ int w4pp_grid(int nwg, bool onetile = false) {
 // issue order, so their 384 KB per tile must drain within two K-tiles (r02 A/B: out-proj 572 vs
 // 593 TF/s, c_proj 1037 vs 1025; with the stores ablated 855 / 1204, profiles/r02).
 // CE_GEMM_AUTO=0 pins SCHED 1, =2 sends every large grid to SCHED 11, =3 every residual-free one.
-int g_auto = -1;
-int gemm_auto() {
-    if (g_auto < 0) {
-        const char* e = getenv("CE_GEMM_AUTO");
-        g_auto = e ? atoi(e) : 1;
-        if (g_auto < 0 || g_auto > 3) g_auto = 1;
-    }
-    return g_auto;
-}
+std::atomic<int> g_auto{kKnobUnset};
+int auto_env() { const int a = env_int("CE_GEMM_AUTO", 1); return (a < 0 || a > 3) ? 1 : a; }
+int gemm_auto() { return knob_get(g_auto, auto_env); }
 bool auto_w4pp(const GemmParams& p, int act, bool resid) {
-    const int on = gemm_auto();
-    if (!on || gemm_sched() != 1) return false;
-    if (p.onetile) return !resid && (act == ACT_NONE || (gemm_variant() & GEMM_VAR_W4_EPI2) != 0);
+    const int on = p.kn.autom;
+    if (!on || p.kn.sched != 1) return false;
+    if (p.onetile) return !resid && (act == ACT_NONE || (p.variant & GEMM_VAR_W4_EPI2) != 0);
     // enough tiles that the persistent grid's last-round imbalance stays small (small grids keep
     // SCHED 1 and its split-K tail)
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
@@ -2608,7 +2575,7 @@ bool auto_w4pp(const GemmParams& p, int act, bool resid) {
     if (on == 2) return true;
     if (on == 3) return !resid;
     if (resid) return false;
-    return act == ACT_NONE || (gemm_variant() & GEMM_VAR_W4_EPI2) != 0;
+    return act == ACT_NONE || (p.variant & GEMM_VAR_W4_EPI2) != 0;
 }
 
 // Launch counters per kernel path (ce_gemm_path_counts): lets the parity tests assert that the
@@ -2622,7 +2589,7 @@ inline void count_path(int path) { g_path[path].fetch_add(1, std::memory_order_r
 // b + 8 share an XCD) start their first tile late
 void set_stagger_1(GemmParams& p, int nwg) {
     if (nwg <= 2 * num_cus()) return;
-    p.stagger = gemm_stagger();
+    p.stagger = p.kn.stagger;
     p.stagger_lo = 0;
     p.stagger_hi = num_cus();
     p.stagger_bit = 3;
@@ -2632,29 +2599,29 @@ void set_stagger_1(GemmParams& p, int nwg) {
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 bool db_ok(const GemmParams& p) {
     if constexpr (!OUT_BF16 || HAS_RESID || !(EPI == EPI_PLAIN || EPI == EPI_LN_FOLD)) return false;
-    else return gemm_sched() == 13 && p.N % 128 == 0 && p.K >= 16 * BK && !p.m_dev && !p.onetile && p.grp == 0;
+    else return p.kn.sched == 13 && p.N % 128 == 0 && p.K >= 16 * BK && !p.m_dev && !p.onetile && p.grp == 0;
 }
 
 template <int ACT, int EPI>
 hipError_t launch_db(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
-    p.gm = gemm_groupm();
+    p.gm = p.kn.groupm;
     p.tail = 0;
     p.split = 1;
     const int nwg = ((p.M + BM - 1) / BM) * (p.N / 128);
     count_path(GEMM_PATH_OTHER);
-    return launch_gemm_db(p, ACT, EPI, w4pp_grid(nwg), s);
+    return launch_gemm_db(p, ACT, EPI, w4pp_grid(p, nwg), s);
 }
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_w2(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
-    p.gm = gemm_groupm();
+    p.gm = p.kn.groupm;
     p.tail = 0;
     p.split = 1;
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + W2_BN - 1) / W2_BN);
     if (nwg > 2 * num_cus()) {     // the second workgroup of each CU starts half a tile late
-        p.stagger = gemm_stagger();
+        p.stagger = p.kn.stagger;
         p.stagger_lo = num_cus();
         p.stagger_hi = 2 * num_cus();
         p.stagger_bit = -1;
@@ -2674,27 +2641,27 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         // a grid of >= 2 tiles per CU (no split-K tail); CE_GEMM_AUTO=0 or a pinned schedule keeps
         // SCHED 1 (r02 A/B at B = 256: out-proj 682 vs 589 TF/s, c_proj 1,092 vs 995)
         const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
-        if ((gemm_variant() & GEMM_VAR_W4_RHL) && gemm_auto() != 0 && gemm_sched() == 1 && p.N % BN == 0 &&
+        if ((p.variant & GEMM_VAR_W4_RHL) && p.kn.autom != 0 && p.kn.sched == 1 && p.N % BN == 0 &&
             p.K >= 2 * BK && (nwg >= 2 * num_cus() || p.onetile)) {
-            p.gm = gemm_groupm();
-            p.stagger = gemm_stagger();
-            plan_tail_rhl(p, nwg, w4pp_grid(nwg, p.onetile));
-            const int abl = ((gemm_variant() & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((gemm_variant() & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
-            const int ex = ((gemm_variant() & GEMM_VAR_RHL_EARLY67) ? 16 : 0) | ((gemm_variant() & GEMM_VAR_RHL_NOREAD2) ? 32 : 0);
-            if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 16)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<20>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 32)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<36>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && ex == 48)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<52>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD) && (gemm_variant() & GEMM_VAR_RHL_DRAIN))
-                hipLaunchKernelGGL(gemm_w4_resid_hl<12>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (gemm_variant() & GEMM_VAR_RHL_DMA_SPREAD))
-                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
-            else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
-            else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(nwg)), dim3(256), 0, s, p);
+            p.gm = p.kn.groupm;
+            p.stagger = p.kn.stagger;
+            plan_tail_rhl(p, nwg, w4pp_grid(p, nwg, p.onetile));
+            const int abl = ((p.variant & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((p.variant & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
+            const int ex = ((p.variant & GEMM_VAR_RHL_EARLY67) ? 16 : 0) | ((p.variant & GEMM_VAR_RHL_NOREAD2) ? 32 : 0);
+            if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 16)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<20>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 32)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<36>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 48)
+                hipLaunchKernelGGL(gemm_w4_resid_hl<52>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && (p.variant & GEMM_VAR_RHL_DRAIN))
+                hipLaunchKernelGGL(gemm_w4_resid_hl<12>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD))
+                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
+            else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
+            else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
             count_path(GEMM_PATH_W4PP + EPI_LN_STATS);
             if (p.tail > 0) {
                 GemmParams q = p;
@@ -2710,23 +2677,23 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     }
     if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
         if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p)) return launch_db<ACT, EPI>(p, s);
-    if (!HL && gemm_sched() == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
-    if (!HL && (gemm_sched() == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
-        p.gm = gemm_groupm();
-        p.stagger = gemm_stagger();
+    if (!HL && p.kn.sched == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
+    if (!HL && (p.kn.sched == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
+        p.gm = p.kn.groupm;
+        p.stagger = p.kn.stagger;
         const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-        const int grid = w4pp_grid(nwg, p.onetile);
+        const int grid = w4pp_grid(p, nwg, p.onetile);
         plan_tail_w4(p, nwg, grid);
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-            (gemm_variant() & GEMM_VAR_W4_SPREAD12))
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+            (p.variant & GEMM_VAR_W4_SPREAD12))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 7>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (gemm_variant() & GEMM_VAR_W4_SPREAD8))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (p.variant & GEMM_VAR_W4_SPREAD8))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 11>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (gemm_variant() & GEMM_VAR_W4_SPREAD_EVEN))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (p.variant & GEMM_VAR_W4_SPREAD_EVEN))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 19>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 3>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(grid), dim3(256), 0, s, p);
@@ -2743,7 +2710,7 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    p.gm = gemm_groupm();
+    p.gm = p.kn.groupm;
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     p.tail = 0;
     p.split = 1;
@@ -2762,14 +2729,25 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The pre-activation copy (GemmParams::pre_out) is written only by the four-wave persistent kernel's
+// one-wave-per-SIMD bf16 epilogue (w4_epilogue_bf16_n, EPI_PLAIN with an activation) over every tile:
+// no split-K tail (its tiles run on SCHED 1, which has no pre_out store), no one-tile grid.
+// launch_gemm routes pre_out launches through here only when this holds, and launch_t rejects any
+// launch whose chosen path would leave pre_out unwritten (the backward would read stale values).
+bool pre_out_fused(const GemmParams& p, int act) {
+    return act != ACT_NONE && !p.onetile && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
+           !(p.variant & GEMM_VAR_W4_TAIL);
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
-    p.gm = gemm_groupm();
+    p.gm = p.kn.groupm;
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    if (p.pre_out && !(OUT_BF16 && !HAS_RESID && pre_out_fused(p, ACT))) return hipErrorInvalidValue;
     if constexpr (OUT_BF16 && !HAS_RESID)
         if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p)) return launch_db<ACT, EPI_PLAIN>(p, s);
-    const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : gemm_sched();
+    const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : p.kn.sched;
     if (sc == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
     p.tail = 0;
     p.split = 1;
@@ -2778,7 +2756,7 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         plan_tail(p, nwg);
         if (p.tail > 0) {
             const int grid = nwg - p.tail + p.tail * p.split;
-            if (HAS_RESID && g_ring == 2)
+            if (HAS_RESID && p.kn.ring == 2)
                 hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(grid), dim3(NTHREADS), 0, s, p);
             else
                 hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(grid), dim3(NTHREADS), 0, s, p);
@@ -2796,19 +2774,20 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         grid = grid < need ? grid : need;
         hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
     } else if (sc == 11) {
-        p.stagger = gemm_stagger();
-        const int grid = w4pp_grid(nwg, p.onetile);
+        p.stagger = p.kn.stagger;
+        const int grid = w4pp_grid(p, nwg, p.onetile);
         plan_tail_w4(p, nwg, grid);
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-            (gemm_variant() & GEMM_VAR_W4_SPREAD12))
+        if (p.pre_out && (p.tail > 0 || !w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))) return hipErrorInvalidValue;
+        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+            (p.variant & GEMM_VAR_W4_SPREAD12))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 7>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (gemm_variant() & GEMM_VAR_W4_SPREAD8))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (p.variant & GEMM_VAR_W4_SPREAD8))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 11>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (gemm_variant() & GEMM_VAR_W4_SPREAD_EVEN))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
+                 (p.variant & GEMM_VAR_W4_SPREAD_EVEN))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 19>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (gemm_variant() & GEMM_VAR_W4_DMA_SPREAD))
+        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
         else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
             hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(grid), dim3(256), 0, s, p);
@@ -2827,11 +2806,11 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
         hipLaunchKernelGGL((gemm_bf16_w4<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
     else if (sc == 0)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && g_ring == 2)   // residual prefetch-depth A/B (bench_kernels)
+    else if (sc == 1 && HAS_RESID && p.kn.ring == 2)   // residual prefetch-depth A/B (bench_kernels)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && g_ring == 3)
+    else if (sc == 1 && HAS_RESID && p.kn.ring == 3)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 3>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && g_ring == 5)
+    else if (sc == 1 && HAS_RESID && p.kn.ring == 5)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 5>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     else if (sc == 1)
         hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
@@ -2885,8 +2864,7 @@ int set_gemm_schedule(int v) {
     const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff, st = (v >> 24) & 0x7f;
     if (ring >= 2 && ring <= 5) g_ring = ring;
     if (st) g_stagger = st - 1;
-    g_sched = (sc == 0 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 || sc == 11 ||
-               sc == 12 || sc == 13) ? sc : 1;
+    g_sched = sched_ok(sc) ? sc : 1;
     if (gm) g_groupm = gm <= 64 ? gm : 1;
     return prev;
 }
@@ -2903,12 +2881,18 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
     p.trace = g_trace;
     p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
     p.variant = gemm_variant();
+    p.kn.sched = gemm_sched();
+    p.kn.autom = gemm_auto();
+    p.kn.splitk = splitk_enabled() ? 1 : 0;
+    p.kn.groupm = gemm_groupm();
+    p.kn.stagger = gemm_stagger();
+    p.kn.ring = g_ring.load();
     p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.m_dev) {
         // packed rows: the folded-tower epilogues on one tile per workgroup, no split-K; only the default
         // schedule's kernels clip at the device row count (run_text turns the packing off otherwise)
-        if ((epi != EPI_LN_FOLD && epi != EPI_LN_STATS_HL) || gemm_sched() != 1) return hipErrorInvalidValue;
+        if ((epi != EPI_LN_FOLD && epi != EPI_LN_STATS_HL) || p.kn.sched != 1) return hipErrorInvalidValue;
         p.onetile = 1;
         p.part = nullptr;
         p.part_elems = 0;
@@ -2921,9 +2905,7 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
         // activation kernel forms out = act(pre)
         if (act == ACT_NONE || !out_bf16 || res || epi != EPI_PLAIN || p.grp || p.m_dev || p.ldo != p.N)
             return hipErrorInvalidValue;
-        const bool fused = !p.onetile && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
-                           !(p.variant & GEMM_VAR_W4_TAIL);
-        if (!fused) {
+        if (!pre_out_fused(p, act)) {
             GemmParams q = p0;
             q.out = p.pre_out;
             q.pre_out = nullptr;

@@ -31,6 +31,7 @@
 //    (deterministic), which applies the row scale.  split == 1 stores C directly.
 #include "ce_device.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -284,18 +285,7 @@ __global__ __launch_bounds__(256) void gemm_tn_fixup(TnParams p) {
     *reinterpret_cast<float4*>(p.C + (long)m * p.ldc + n) = make_float4(s.x * sc, s.y * sc, s.z * sc, s.w * sc);
 }
 
-int g_tn_cus = 0;
-int tn_num_cus() {
-    if (g_tn_cus <= 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            g_tn_cus = n;
-        else
-            g_tn_cus = 256;
-    }
-    return g_tn_cus;
-}
+int tn_num_cus() { return device_cus(); }     // cached per device (knobs.h)
 
 }  // namespace
 

@@ -12,6 +12,7 @@
 //    below sigma, divide by the row sum (+1e-8)  (pacl.py:462-471).
 #include "ce_device.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 namespace ce {
 namespace {
@@ -524,12 +525,12 @@ __global__ __launch_bounds__(256) void sparc_weights_k(float* sim, long rows, in
 // f32 GEMM variant: 0 = the 64 x 64 scalar-staged kernel; 1 (default) = the register-blocked 96 x 128
 // kernel; 2 = as 1, with the short-M 80 x 192 kernel for batched products of M <= 80 rows (measured
 // slower at the C5 shapes: sparc_sim 51.5 vs 62.9 TF/s, sparc_group 59.3 vs 71.1; kept for A/B)
-int g_fgemm2 = 1;
+std::atomic<int> g_fgemm2{1};     // A/B knob (knobs.h: process-wide atomic)
 
 }  // namespace
 
 int set_fgemm_variant(int v) {
-    const int prev = g_fgemm2;
+    const int prev = g_fgemm2.load();
     g_fgemm2 = v < 0 ? 0 : v > 2 ? 2 : v;
     return prev;
 }
@@ -541,13 +542,14 @@ hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s) {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     const bool vec = p.K % 4 == 0 && p.lda % 4 == 0 && p.ldb % 4 == 0 && p.sA % 4 == 0 && p.sB % 4 == 0 &&
                      al(p.A) && al(p.B) && (b_nk || p.N % 4 == 0);
-    if (vec && g_fgemm2 == 2 && p.M <= G3_BM && p.N >= G3_BN && p.batch > 1) {
+    const int fv = g_fgemm2.load(std::memory_order_acquire);
+    if (vec && fv == 2 && p.M <= G3_BM && p.N >= G3_BN && p.batch > 1) {
         const dim3 grid((p.N + G3_BN - 1) / G3_BN, 1, p.batch);
         if (b_nk) hipLaunchKernelGGL(fgemm3_k<true>, grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL(fgemm3_k<false>, grid, dim3(256), 0, s, p);
         return hipGetLastError();
     }
-    if (vec && g_fgemm2) {
+    if (vec && fv) {
         const dim3 grid((p.N + G2_BN - 1) / G2_BN, (p.M + G2_BM - 1) / G2_BM, p.batch);
         if (b_nk) hipLaunchKernelGGL(fgemm2_k<true>, grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL(fgemm2_k<false>, grid, dim3(256), 0, s, p);

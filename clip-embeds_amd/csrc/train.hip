@@ -13,6 +13,7 @@
 //   AdamW                      torch.optim.AdamW (open_clip_train/main.py: betas, eps, wd groups)
 #include "ce_device.h"
 #include "ce_kernels.h"
+#include "knobs.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -599,14 +600,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv,
     }
 }
 
-int g_attn_bwd_var = -1;
-int attn_bwd_variant() {
-    if (g_attn_bwd_var < 0) {
-        const char* e = getenv("CE_ATTN_BWD");
-        g_attn_bwd_var = (e && atoi(e) == 1) ? 1 : 2;
-    }
-    return g_attn_bwd_var;
-}
+std::atomic<int> g_attn_bwd_var{kKnobUnset};     // A/B knob (knobs.h)
+int attn_bwd_env() { return env_int("CE_ATTN_BWD", 2) == 1 ? 1 : 2; }
+int attn_bwd_variant() { return knob_get(g_attn_bwd_var, attn_bwd_env); }
 
 // ---------------------------------------------------------------------------------------------
 // Token-embedding gradient, deterministic: (id, row) pairs sorted by id (stable radix sort), one
@@ -928,17 +924,18 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
                                 int B, int L, int H, bool causal, hipStream_t s, float* dbias, float* bpart,
                                 float* scratch) {
     if (L <= 0 || L > AB_L || B <= 0 || !lse || (dbias && (!bpart || !scratch))) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
+    // dynamic-LDS opt-in, once per device (several host threads may drive several devices)
+    static std::atomic<bool> attr[kMaxDevices], attr2[kMaxDevices];
+    const int dev = current_device();
+    if (!attr[dev].load(std::memory_order_acquire)) {
         (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
-        attr = true;
+        attr[dev].store(true, std::memory_order_release);
     }
     if (attn_bwd_variant() == 2) {
-        static bool attr2 = false;
-        if (!attr2) {
+        if (!attr2[dev].load(std::memory_order_acquire)) {
             (void)hipFuncSetAttribute((const void*)attn_bwd2_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kAttnBwd2Lds);
-            attr2 = true;
+            attr2[dev].store(true, std::memory_order_release);
         }
         hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse, L,
                            H, causal ? 1 : 0, dbias ? bpart : nullptr);
@@ -954,7 +951,7 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
 
 int set_attn_bwd_variant(int v) {
     const int prev = attn_bwd_variant();
-    g_attn_bwd_var = v == 1 ? 1 : 2;
+    g_attn_bwd_var.store(v == 1 ? 1 : 2);
     return prev;
 }
 

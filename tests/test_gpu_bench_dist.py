@@ -2,7 +2,9 @@
 (torch.distributed.run via bench.py --gpus 2), both on cuda:0 over gloo (RCCL runs one rank per
 device).  Exercises what a multi-GPU run executes besides the collectives' transport: the rank
 setup, the barrier + max-over-ranks timing, the embedding all-gather and local logits (clip), the
-global-batch SparcLoss / PACL ClipLoss exchange (sparc, pacl), rank 0's single JSON line.  Not a
+global-batch SparcLoss / PACL ClipLoss exchange (sparc, pacl), the NegCLIP trainer's all-gathers of
+features and sizes, reduce-scatter of their gradient and DDP all-reduce with the engine's text-tower
+backward (negclip, BASELINE configs[3]), rank 0's single JSON line.  Not a
 scaling measurement (the two ranks share one GPU)."""
 import json
 import os
@@ -15,7 +17,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("workload,batch", [("clip", 16), ("sparc", 8), ("pacl", 8)])
+@pytest.mark.parametrize("workload,batch", [("clip", 16), ("sparc", 8), ("pacl", 8), ("negclip", 16)])
 def test_bench_two_ranks_shared_device(workload, batch):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--share-device", "--dist-backend", "gloo",
            "--workload", workload, "--batch", str(batch), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
