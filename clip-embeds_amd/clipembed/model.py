@@ -51,6 +51,7 @@ class Engine:
         h = ctypes.c_void_p()
         _lib.call("ce_create", ctypes.byref(c), device_index, ctypes.byref(h))
         self.h = h
+        self.timing = False
 
     def close(self):
         if self.h:
@@ -124,6 +125,7 @@ class Engine:
         """Bracket kernel launches with HIP events (all tags, or only the launches tagged `only`)."""
         _lib.call("ce_set_kernel_timing_filter", self.h, only.encode())
         _lib.call("ce_set_kernel_timing", self.h, 1 if on else 0)
+        self.timing = bool(on)
 
     def kernel_stats(self):
         out = []

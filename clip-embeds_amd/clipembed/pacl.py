@@ -215,13 +215,37 @@ class sparc_rope(sparc):
     rope = _lib.CE_ROPE_BEFORE
 
 
-def _all_gather_rows(x: torch.Tensor, world_size: int) -> torch.Tensor:
-    """Every rank's [B, D] rows concatenated in rank order (torch.distributed: RCCL over xGMI with
-    the "nccl" backend; gloo in the CPU / single-GPU tests)."""
+def _all_gather_rows(x: torch.Tensor, world_size: int, rank: int):
+    """Every rank's [B_r, D] rows concatenated in rank order, and this rank's first row in it
+    (torch.distributed: RCCL over xGMI with the "nccl" backend; gloo in the CPU / single-GPU tests).
+    The ranks may hold different B_r (an uneven last batch; nn.DataParallel's scatter splits unevenly
+    too): the sizes are gathered first and the rows padded to the largest, as open_clip's
+    gather_features_diffsize does (loss.py:67-87)."""
     import torch.distributed as dist
-    parts = [torch.empty_like(x) for _ in range(world_size)]
-    dist.all_gather(parts, x.contiguous())
-    return torch.cat(parts, dim=0)
+    x = x.contiguous()
+    n = torch.tensor([x.shape[0]], device=x.device, dtype=torch.int64)
+    sizes = [torch.empty_like(n) for _ in range(world_size)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s) for s in sizes]
+    mx = max(sizes)
+    if all(s == mx for s in sizes):
+        parts = [torch.empty_like(x) for _ in range(world_size)]
+        dist.all_gather(parts, x)
+    else:
+        pad = torch.zeros((mx,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        pad[:x.shape[0]] = x
+        parts = [torch.empty_like(pad) for _ in range(world_size)]
+        dist.all_gather(parts, pad)
+        parts = [p[:s] for p, s in zip(parts, sizes)]
+    return torch.cat(parts, dim=0), sum(sizes[:rank])
+
+
+def _value_only(name: str, *tensors):
+    """The sharded losses return the reference's global VALUE (logging, evaluation); their all-gather
+    is not differentiable, so a caller that needs gradients must not get a silently detached loss."""
+    if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
+        raise RuntimeError(f"{name}(rank=, world_size=) returns the global loss value only (no autograd "
+                           "through the all-gather); call it under torch.no_grad() or on detached inputs")
 
 
 def _all_reduce_sum(x: torch.Tensor) -> torch.Tensor:
@@ -237,10 +261,12 @@ class ClipLoss(torch.nn.Module):
     rank / world_size (not in the reference's signature, whose callers are single-process): the
     batch is sharded over data-parallel ranks, and the value is the reference's loss over the WHOLE
     batch, as train_pacl.py:34-36,95 computes it after nn.DataParallel gathers every replica's
-    outputs to one device.  The ranks all-gather the [B, D] features (equal B per rank), each takes
-    the CE sums of its own rows of the global logits both ways (ce_contrastive_loss_partial), one
-    all-reduce adds them, ce_loss_combine divides by the global batch.  Every rank returns the same
-    value."""
+    outputs to one device.  The ranks all-gather the [B_r, D] features (B_r may differ per rank:
+    sizes first, padded rows), each takes the CE sums of its own rows of the global logits both ways
+    (ce_contrastive_loss_partial), one all-reduce adds them, ce_loss_combine divides by the global
+    batch.  Every rank returns the same value.  The sharded path returns the VALUE only (the
+    all-gather is not differentiable): with inputs that require grad it raises instead of returning
+    a detached loss; the single-process path is @no_grad as before (the engine computes no autograd)."""
 
     def __init__(self, temperature: float, engine=None, rank: int = 0, world_size: int = 1):
         super().__init__()
@@ -285,8 +311,13 @@ class ClipLoss(torch.nn.Module):
                   float(local_weight), _ptr(out))
         return out
 
-    @torch.no_grad()
     def forward(self, image_features, text_features):
+        if self.world_size > 1:
+            _value_only("ClipLoss", image_features, text_features)
+        with torch.no_grad():
+            return self._forward(image_features, text_features)
+
+    def _forward(self, image_features, text_features):
         e = self._engine(image_features)
         if self.world_size > 1:
             a = image_features.float().contiguous()
@@ -294,9 +325,9 @@ class ClipLoss(torch.nn.Module):
             B = a.shape[0]
             if b.shape[0] != B:
                 raise ValueError(f"ClipLoss: {B} image rows but {b.shape[0]} text rows")
-            img_all = _all_gather_rows(a, self.world_size)
-            txt_all = _all_gather_rows(b, self.world_size)
-            parts = _all_reduce_sum(self._contrastive_parts(e, img_all, txt_all, self.rank * B, B))
+            img_all, row0 = _all_gather_rows(a, self.world_size, self.rank)
+            txt_all, _ = _all_gather_rows(b, self.world_size, self.rank)
+            parts = _all_reduce_sum(self._contrastive_parts(e, img_all, txt_all, row0, B))
             return self._combine(e, parts, img_all.shape[0], 1.0, 0.0)
         lpi, lpt = self.get_logits(image_features, text_features)
         labels = self.get_ground_truth(image_features.device, lpi.shape[0])
@@ -334,8 +365,13 @@ class SparcLoss(ClipLoss):
                   row0, _ptr(lt), _ptr(g), _ptr(m), B, T, D, 1.0 / float(self.logit_scale), _ptr(parts))
         return parts
 
-    @torch.no_grad()
     def forward(self, v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask):
+        if self.world_size > 1:
+            _value_only("SparcLoss", v_patch_embed, l_token_embed, l_grouped_v_patch_embed)
+        with torch.no_grad():
+            return self._forward(v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask)
+
+    def _forward(self, v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask):
         e = self._engine(v_patch_embed)
         v = v_patch_embed.float().contiguous()
         lt = l_token_embed.float().contiguous()
@@ -348,9 +384,9 @@ class SparcLoss(ClipLoss):
                              f"g {tuple(g.shape)} mask {tuple(m.shape)}")
         if self.world_size > 1:
             gi, gt = self._means(e, v, lt)
-            img_all = _all_gather_rows(gi, self.world_size)
-            txt_all = _all_gather_rows(gt, self.world_size)
-            parts = _all_reduce_sum(self._sparc_parts(e, img_all, txt_all, self.rank * B, lt, g, m))
+            img_all, row0 = _all_gather_rows(gi, self.world_size, self.rank)
+            txt_all, _ = _all_gather_rows(gt, self.world_size, self.rank)
+            parts = _all_reduce_sum(self._sparc_parts(e, img_all, txt_all, row0, lt, g, m))
             return self._combine(e, parts, img_all.shape[0], self.global_weight, self.local_weight)
         out = torch.empty((), device=v.device, dtype=torch.float32)
         _lib.call("ce_sparc_loss", e.h, _stream(e.device), _ptr(v), _ptr(lt), _ptr(g), _ptr(m), B, P, T, D,

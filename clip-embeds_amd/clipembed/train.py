@@ -200,6 +200,11 @@ class TextTowerTrainer:
         if not self.overlap_text:
             img = self.model.encode_image(images, normalize=True)
             return self.compute_grads_from_features(img, texts)
+        if self.e.timing:
+            # one handle on two concurrent streams: its per-kernel event brackets and the profile
+            # pass's host readbacks are not stream-aware, so timings would be misattributed
+            raise RuntimeError("TextTowerTrainer.overlap_text cannot run with engine kernel timing on "
+                               "(Engine.set_timing): turn one of them off")
         main = torch.cuda.current_stream(self.dev)
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.dev)

@@ -735,7 +735,10 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
             case 9: CE_ATTN_LAUNCH(false, 9); break;
             case 13: CE_ATTN_LAUNCH(false, 13); break;
             case 1: CE_ATTN_LAUNCH(false, 1); break;
-            default: CE_ATTN_LAUNCH(false, 381); break;
+            default:     // unreachable through set_attn_variant; keep the CLSK guard of vv anyway
+                if ((L - 1) % KBLK == 0 && L > 1) CE_ATTN_LAUNCH(false, 381);
+                else CE_ATTN_LAUNCH(false, 125);
+                break;
         }
     }
 #undef CE_ATTN_LAUNCH

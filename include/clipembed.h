@@ -17,7 +17,11 @@
  *  - One handle per device.  A handle may be used from any host thread, but calls on one
  *    handle must not overlap in time (they share the handle's workspace); handles on
  *    different devices are fully independent (this is how nn.DataParallel-style callers
- *    drive 8 GPUs from 8 host threads).
+ *    drive 8 GPUs from 8 host threads), and so are several handles on one device.
+ *  - The library keeps no mutable state outside the handles except the ce_set_* A/B knobs
+ *    that take no handle (process-wide atomics, read once per launch; they affect every
+ *    handle) and per-device caches keyed by device ordinal (CU count, the kernel-level
+ *    entry points' split-K workspace, allocated under a lock).
  */
 #ifndef CLIPEMBED_H
 #define CLIPEMBED_H

@@ -143,7 +143,7 @@ def test_train_feature_grad_two_ranks(golden):
         np.testing.assert_allclose(got[r]["dtxt"], g[f"dtxt_r{r}"], rtol=1e-4, atol=1e-7)
 
 
-def _loss_worker(rank, world, port, q):
+def _loss_worker(rank, world, port, q, uneven=None):
     """clipembed.pacl.SparcLoss / ClipLoss(rank, world_size) on 2 gloo ranks: the product's exchange
     (all-gather of the [B,768] means / features, shard row offsets, all-reduce of the 5 partial sums)
     with the oracle's arithmetic in place of the engine calls (test double: no device here)."""
@@ -181,10 +181,17 @@ def _loss_worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    v, l, g, m = (torch.from_numpy(x) for x in sparc_shard(rank))
-    img, txt = (torch.from_numpy(x) for x in pacl_shard(rank))
+    n = uneven[rank] if uneven else 4
+    v, l, g, m = (torch.from_numpy(x[:n]) for x in sparc_shard(rank))
+    img, txt = (torch.from_numpy(x[:n]) for x in pacl_shard(rank))
     res = {"sparc": float(CpuSparcLoss(0.1, rank=rank, world_size=world)(v, l, g, m)),
            "pacl": float(CpuClipLoss(0.1, rank=rank, world_size=world)(img, txt))}
+    if rank == 0:     # the sharded loss is value-only: inputs that require grad are refused
+        try:
+            CpuClipLoss(0.1, rank=rank, world_size=world)(img.clone().requires_grad_(), txt)
+            res["grad_refused"] = False
+        except RuntimeError:
+            res["grad_refused"] = True
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -209,6 +216,39 @@ def test_sparc_pacl_global_loss_two_ranks(golden):
         np.testing.assert_allclose(got[r]["pacl"], float(g["pacl_global"]), rtol=1e-5, err_msg=f"rank {r}")
         assert abs(got[r]["sparc"] - float(g[f"sparc_shard_r{r}"])) > 0.05     # not the shard-local value
         assert abs(got[r]["pacl"] - float(g[f"pacl_shard_r{r}"])) > 0.05
+
+
+def test_sparc_pacl_global_loss_uneven_shards():
+    """Ranks holding different batch sizes (4 and 2 samples: an uneven last batch; nn.DataParallel
+    scatters unevenly too): sizes are gathered first, rows padded, and every rank returns the loss
+    over the whole 6-sample batch (the oracle, pinned to the reference by the tests above, on the
+    concatenated batch)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from dist_inputs import pacl_shard, sparc_shard
+    from oracle import clip_oracle as O
+    sizes = (4, 2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loss_worker, args=(r, 2, port, q, sizes)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sh = [[x[:n] for x in sparc_shard(r)] for r, n in enumerate(sizes)]
+    v, l, g, m = (np.concatenate([s[k] for s in sh]) for k in range(4))
+    gi, gt = O.sparc_loss_means(v, l)
+    want_sparc = O.loss_combine(O.sparc_loss_parts(gi, gt, 0, l, g, m, 0.1), 6, 0.5, 1.0)
+    ph = [[x[:n] for x in pacl_shard(r)] for r, n in enumerate(sizes)]
+    img, txt = (np.concatenate([s[k] for s in ph]) for k in range(2))
+    want_pacl = O.loss_combine(O.contrastive_loss_parts(img, txt, 0, 6, 10.0), 6, 1.0, 0.0)
+    for r in range(2):
+        np.testing.assert_allclose(got[r]["sparc"], want_sparc, rtol=1e-5, err_msg=f"rank {r}")
+        np.testing.assert_allclose(got[r]["pacl"], want_pacl, rtol=1e-5, err_msg=f"rank {r}")
+    assert got[0]["grad_refused"]
 
 
 def test_oracle_shard_parts_add_up(golden):
