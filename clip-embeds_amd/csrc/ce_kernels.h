@@ -72,6 +72,10 @@ hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t 
 // SCHED 13 (gemm_db.hip): bf16 output without residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0,
 // K >= 1024; `grid` persistent workgroups (p.gm set by the caller)
 hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipStream_t s);
+// SCHED 14 (gemm_w2b.hip): two independent 256 x 128-tile workgroups per CU; bf16 output without
+// residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0, K % 32 == 0 (p.gm set by the caller)
+bool gemm_w2b_supported(const GemmParams& p, int epi, bool out_bf16, bool resid);
+hipError_t launch_gemm_w2b(const GemmParams& p, int act, int epi, hipStream_t s);
 // (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
 // combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
 // (m_dev: packed rows, only the first *m_dev of the `rows` are live)

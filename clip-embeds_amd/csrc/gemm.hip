@@ -2433,7 +2433,7 @@ int gemm_variant() { return knob_get(g_variant, variant_env); }
 
 bool sched_ok(int sc) {
     return sc == 0 || sc == 1 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 ||
-           sc == 11 || sc == 12 || sc == 13;
+           sc == 11 || sc == 12 || sc == 13 || sc == 14;
 }
 std::atomic<int> g_sched{kKnobUnset};
 std::atomic<int> g_ring{CE_RESID_RING};     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
@@ -2677,6 +2677,12 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     }
     if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
         if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p)) return launch_db<ACT, EPI>(p, s);
+    if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
+        if (p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, EPI, true, false)) {
+            p.gm = p.kn.groupm;
+            count_path(GEMM_PATH_W2 + EPI);
+            return launch_gemm_w2b(p, ACT, EPI, s);
+        }
     if (!HL && p.kn.sched == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     if (!HL && (p.kn.sched == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
         p.gm = p.kn.groupm;
@@ -2747,6 +2753,11 @@ hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     if (p.pre_out && !(OUT_BF16 && !HAS_RESID && pre_out_fused(p, ACT))) return hipErrorInvalidValue;
     if constexpr (OUT_BF16 && !HAS_RESID)
         if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p)) return launch_db<ACT, EPI_PLAIN>(p, s);
+    if constexpr (OUT_BF16 && !HAS_RESID)
+        if (p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, EPI_PLAIN, true, false)) {
+            count_path(GEMM_PATH_W2);
+            return launch_gemm_w2b(p, ACT, EPI_PLAIN, s);
+        }
     const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : p.kn.sched;
     if (sc == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
     p.tail = 0;
@@ -2897,8 +2908,10 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
         p.part = nullptr;
         p.part_elems = 0;
     }
-    if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     const bool res = p.resid != nullptr;
+    // SCHED 14 steps K by 32: it takes K % 64 == 32 too (every other path needs K % 64 == 0)
+    const bool w2b_k = p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, epi, out_bf16, res);
+    if ((p.K % BK != 0 && !w2b_k) || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     if (p.pre_out) {
         // pre-activation copy: written by the four-wave kernel's one-wave-per-SIMD epilogue (the
         // default policy's path for this GEMM); on any other path the GEMM writes pre and the

@@ -209,8 +209,11 @@ def test_negclip_step_two_ranks_equals_one_rank_on_concatenated_batch():
         # both ranks hold the same averaged gradient and apply the same update
         np.testing.assert_array_equal(two["g_sample"], got[0]["g_sample"])
         np.testing.assert_array_equal(two["u_sample"], got[0]["u_sample"])
-        # first AdamW step: update = -lr * g / (|g| + eps) (+ decay): equal wherever |g| is clear of eps
-        big = np.abs(one["g_sample"]) > 1e-5
-        assert big.sum() > 100
+        # first AdamW step: update = -lr * g / (|g| + eps) (+ decay): equal wherever g is clear of eps and
+        # of the bf16 GEMMs' noise, which is relative to the tensor's scale, not to each element
+        # (|g| >= 1e-4 = 100 eps: there du/u = eps / (|g| + eps) * dg/g <= 1e-2 dg/g)
+        gs = np.abs(one["g_sample"])
+        big = gs > max(1e-4, float(np.quantile(gs, 0.9)))
+        assert big.sum() >= 50
         np.testing.assert_allclose(two["u_sample"][big], one["u_sample"][big], rtol=2e-2, atol=1e-7)
         np.testing.assert_allclose(two["u_ls"], one["u_ls"], rtol=2e-2, atol=1e-7)
