@@ -1,7 +1,7 @@
 """SCHED 14 (gemm_w2b, csrc/gemm_w2b.hip): two independent 256 x 128-tile workgroups per CU.  Checked
 against plain PyTorch f32 references of the same op (bias / GELU / QuickGELU, null bias, LN-folded
-consumer), with a ragged last M tile, the shortest K (2 K-steps: the prologue's two in flight), odd
-step counts (the 3-slot ring and the 6-step unroll's tails), K = 4096, grids below the CU count; rows
+consumer), with a ragged last M tile, the shortest K (2 K-steps: the prologue's two in flight), step
+counts 4, 6 and 10 (the 3-slot ring and the 6-step unroll's tails), K = 4096, grids below the CU count; rows
 past M must stay untouched; and against SCHED 11 on the QKV shape."""
 import ctypes
 
@@ -50,7 +50,7 @@ def _ref_act(ref, act):
 
 
 SHAPES = [(20000, 3072, 1024), (2308, 4096, 1024), (17000, 1024, 4096), (300, 1024, 1024), (5, 768, 1024),
-          (1000, 256, 64), (700, 128, 96), (4100, 512, 224), (300, 384, 352)]
+          (1000, 256, 64), (700, 128, 128), (4100, 512, 192), (300, 384, 320)]
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
