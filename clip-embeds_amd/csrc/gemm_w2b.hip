@@ -97,8 +97,14 @@ __device__ __forceinline__ f32x4 act4(f32x4 v) {
     }
 }
 
-template <int ACT, int EPI>
+// VAR (A/B, GemmParams::variant bits 22-23): 1 = "block" steps: all 12 fragment reads and the 6 DMA
+// pieces right after the barrier, one lgkmcnt(0), then 32 back-to-back MFMAs (a load segment and a
+// compute segment per step, for the CU's other workgroup to interleave with); 2 = s_setprio 1 over the
+// MFMA segment.
+template <int ACT, int EPI, int VAR = 0>
 __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
+    constexpr bool BLOCK = (VAR & 1) != 0;
+    constexpr bool PRIO = (VAR & 2) != 0;
     __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 bw[2][4], ar[3];
+    bf16x8 bw[2][4], ar[BLOCK ? 8 : 3];
 
     // epilogue operands, loaded during the last K-step
     float4 bv[4], cv[4];
@@ -186,6 +192,35 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier();
         const bool pf = t + 2 < nk;
+        if constexpr (BLOCK) {
+            W2B_RD(bw[P][0], wbase, SO + 0 * 1024);
+            W2B_RD(bw[P][1], wbase, SO + 1 * 1024);
+            W2B_RD(bw[P][2], wbase, SO + 2 * 1024);
+            W2B_RD(bw[P][3], wbase, SO + 3 * 1024);
+            W2B_RD(ar[0], abase, SO + 0 * 1024);
+            W2B_RD(ar[1], abase, SO + 1 * 1024);
+            W2B_RD(ar[2 % (BLOCK ? 8 : 3)], abase, SO + 2 * 1024);
+            W2B_RD(ar[3 % (BLOCK ? 8 : 3)], abase, SO + 3 * 1024);
+            W2B_RD(ar[4 % (BLOCK ? 8 : 3)], abase, SO + 4 * 1024);
+            W2B_RD(ar[5 % (BLOCK ? 8 : 3)], abase, SO + 5 * 1024);
+            W2B_RD(ar[6 % (BLOCK ? 8 : 3)], abase, SO + 6 * 1024);
+            W2B_RD(ar[7 % (BLOCK ? 8 : 3)], abase, SO + 7 * 1024);
+            if (pf) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) piece(t + 2, j);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (PRIO) asm volatile("s_setprio 1" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                W2B_MFMA(acc[i][0], bw[P][0], ar[i % (BLOCK ? 8 : 3)]);
+                W2B_MFMA(acc[i][1], bw[P][1], ar[i % (BLOCK ? 8 : 3)]);
+                W2B_MFMA(acc[i][2], bw[P][2], ar[i % (BLOCK ? 8 : 3)]);
+                W2B_MFMA(acc[i][3], bw[P][3], ar[i % (BLOCK ? 8 : 3)]);
+            }
+            if constexpr (PRIO) asm volatile("s_setprio 0" ::: "memory");
+            return;
+        }
         // W fragments 0..3, A fragments 0..1
         W2B_RD(bw[P][0], wbase, SO + 0 * 1024);
         W2B_RD(bw[P][1], wbase, SO + 1 * 1024);
@@ -193,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
         W2B_RD(bw[P][3], wbase, SO + 3 * 1024);
         W2B_RD(ar[0], abase, SO + 0 * 1024);
         W2B_RD(ar[1], abase, SO + 1 * 1024);
+        if constexpr (PRIO) asm volatile("s_setprio 1" ::: "memory");
         static_for<8>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             // fragments of row i landed (row i + 1's read may stay in flight)
@@ -206,6 +242,7 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
             if (i < 6 && pf) piece(t + 2, i);
             W2B_MFMA(acc[i][3], bw[P][3], ar[i % 3]);
         });
+        if constexpr (PRIO) asm volatile("s_setprio 0" ::: "memory");
     };
 
     piece(0, 0); piece(0, 1); piece(0, 2); piece(0, 3); piece(0, 4); piece(0, 5);
@@ -283,7 +320,14 @@ bool gemm_w2b_supported(const GemmParams& p, int epi, bool out_bf16, bool resid)
 hipError_t launch_gemm_w2b(const GemmParams& p, int act, int epi, hipStream_t s) {
     if (!gemm_w2b_supported(p, epi, true, false)) return hipErrorInvalidValue;
     const int nwg = ((p.M + TM - 1) / TM) * (p.N / TN);
-#define W2B_LAUNCH(A_, E_) hipLaunchKernelGGL((gemm_w2b<A_, E_>), dim3(nwg), dim3(256), 0, s, p)
+    const int var = (p.variant >> 22) & 3;
+#define W2B_LAUNCH(A_, E_)                                                                                   \
+    do {                                                                                                  \
+        if (var == 1) hipLaunchKernelGGL((gemm_w2b<A_, E_, 1>), dim3(nwg), dim3(256), 0, s, p);            \
+        else if (var == 2) hipLaunchKernelGGL((gemm_w2b<A_, E_, 2>), dim3(nwg), dim3(256), 0, s, p);       \
+        else if (var == 3) hipLaunchKernelGGL((gemm_w2b<A_, E_, 3>), dim3(nwg), dim3(256), 0, s, p);       \
+        else hipLaunchKernelGGL((gemm_w2b<A_, E_, 0>), dim3(nwg), dim3(256), 0, s, p);                     \
+    } while (0)
     if (epi == EPI_LN_FOLD) {
         if (act == ACT_GELU) W2B_LAUNCH(ACT_GELU, EPI_LN_FOLD);
         else if (act == ACT_QGELU) W2B_LAUNCH(ACT_QGELU, EPI_LN_FOLD);
