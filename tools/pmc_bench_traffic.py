@@ -19,17 +19,34 @@ from collections import defaultdict
 TAGS = {"gemm_fc_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<1, false, true, 2", 65536),
         "gemm_qkv_v": ("void ce::(anonymous namespace)::gemm_bf16_w4pp<0, false, true, 2", 65536),
         "attn_v": ("void ce::(anonymous namespace)::attn_fwd<false", None),
+        "gemm_out_v": ("resid_hl:out", 65536),
+        "gemm_proj_v": ("resid_hl:proj", 65536),
         "pacl_pool": (("void ce::(anonymous namespace)::pacl_pool_part_k", "ce::(anonymous namespace)::pacl_pool_finish_k"),
                       None)}
 
 
+RESID_HL = "void ce::(anonymous namespace)::gemm_w4_resid_hl<"
+
+
 def load(d, counter):
+    """{(kernel, grid): [value per dispatch]}; the staged-residual kernel's dispatches (out-proj and
+    c_proj share its name and grid) are split by dispatch order: each image block launches out-proj
+    before c_proj, so in dispatch order they alternate out, proj, out, proj ..."""
     g = defaultdict(list)
+    hl = []
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if row["Counter_Name"] == counter:
-                    g[(row["Kernel_Name"], int(row["Grid_Size"]))].append(float(row["Counter_Value"]))
+                if row["Counter_Name"] != counter:
+                    continue
+                key = (row["Kernel_Name"], int(row["Grid_Size"]))
+                if key[0].startswith(RESID_HL) and key[1] == 65536:
+                    hl.append((int(row.get("Dispatch_Id", 0)), float(row["Counter_Value"])))
+                else:
+                    g[key].append(float(row["Counter_Value"]))
+    hl.sort()
+    for i, (_, v) in enumerate(hl):
+        g[("resid_hl:" + ("out" if i % 2 == 0 else "proj"), 65536)].append(v)
     return g
 
 
