@@ -193,7 +193,9 @@ def build_clip(args, dev, rank, world):
     # the two towers are independent until the logits: the text tower runs on a second HIP stream
     # so its kernels fill the image tower's partial last rounds and launch gaps (--serial-towers:
     # one stream)
-    side = None if args.serial_towers else torch.cuda.Stream(dev)
+    # --text-priority: the text tower's stream at high priority instead (its small kernels are
+    # dispatched first whenever the image tower's persistent GEMMs free CUs)
+    side = None if args.serial_towers else torch.cuda.Stream(dev, priority=-1 if args.text_priority else 0)
     # --tower-priority: the image tower (the critical path) on a high-priority stream, so the
     # dispatcher prefers its workgroups and the text tower only fills gaps
     hp = torch.cuda.Stream(dev, priority=-1) if (side is not None and args.tower_priority) else None
@@ -380,6 +382,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--serial-towers", action="store_true", help="clip: both towers on one stream")
     ap.add_argument("--tower-priority", action="store_true", help="clip: image tower on a high-priority stream")
+    ap.add_argument("--text-priority", action="store_true", help="clip: text tower on a high-priority stream")
     ap.add_argument("--attn-var", type=int, default=-1, help="attention forward variant for A/B (-1 = default)")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM variant bits for A/B (-1 = default)")
     ap.add_argument("--no-pooled-prune", action="store_true",
