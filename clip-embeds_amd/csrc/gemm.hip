@@ -148,7 +148,12 @@ enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
        GEMM_VAR_RHL_DRAIN = 1 << 19,
        // staged-residual kernel: rows 6-7's residual loaded in the last K-tile (ABL bit 4); staged-row
        // reads kept as single ds_read_b64 (ABL bit 5)
-       GEMM_VAR_RHL_EARLY67 = 1 << 20, GEMM_VAR_RHL_NOREAD2 = 1 << 21 };
+       GEMM_VAR_RHL_EARLY67 = 1 << 20, GEMM_VAR_RHL_NOREAD2 = 1 << 21,
+       // (bits 22-23: SCHED 14 timing variants, gemm_w2b.hip)
+       // the default schedule with the two-workgroup SCHED 14 kernel for: the hi/lo residual GEMMs of
+       // K <= 2048 (out-proj), every hi/lo residual GEMM, the LN-fold GEMMs (QKV / c_fc); big grids only
+       // (not the text tower's one-tile launches)
+       GEMM_VAR_W2B_OUT = 1 << 24, GEMM_VAR_W2B_RESID = 1 << 25, GEMM_VAR_W2B_FOLD = 1 << 26 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \
@@ -2637,6 +2642,13 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     // the hi/lo residual epilogues exist on SCHED 1 (+ its split-K tail) only
     constexpr bool HL = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
     if constexpr (EPI == EPI_LN_STATS_HL) {
+        const bool w2b_pol = p.kn.sched == 1 && p.kn.autom != 0 &&
+                             ((p.variant & GEMM_VAR_W2B_RESID) || ((p.variant & GEMM_VAR_W2B_OUT) && p.K <= 2048));
+        if ((p.kn.sched == 14 || w2b_pol) && !p.onetile && gemm_w2b_supported(p, EPI, false, false)) {
+            p.gm = p.kn.groupm;
+            count_path(GEMM_PATH_W2 + EPI_LN_STATS);
+            return launch_gemm_w2b(p, ACT_NONE, EPI, s);
+        }
         // staged-residual four-wave kernel (default policy): whole 256-column tiles, >= 2 K-tiles,
         // a grid of >= 2 tiles per CU (no split-K tail); CE_GEMM_AUTO=0 or a pinned schedule keeps
         // SCHED 1 (r02 A/B at B = 256: out-proj 682 vs 589 TF/s, c_proj 1,092 vs 995)
@@ -2678,7 +2690,9 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
         if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p)) return launch_db<ACT, EPI>(p, s);
     if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
-        if (p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, EPI, true, false)) {
+        if ((p.kn.sched == 14 || (EPI == EPI_LN_FOLD && p.kn.sched == 1 && p.kn.autom != 0 &&
+                                  (p.variant & GEMM_VAR_W2B_FOLD) && !p.m_dev)) &&
+            !p.onetile && gemm_w2b_supported(p, EPI, true, false)) {
             p.gm = p.kn.groupm;
             count_path(GEMM_PATH_W2 + EPI);
             return launch_gemm_w2b(p, ACT, EPI, s);

@@ -26,7 +26,8 @@
 //  * Epilogue operands (bias, LN-fold column sums, row (mu, rstd)) are loaded into registers after
 //    the K-loop (loading them during the last K-step spilled); bf16 output rows paired by v_permlane16_swap into 16-B stores through a buffer
 //    descriptor clipped at row M (rows past M dropped).
-// Supported: bf16 output, no residual, EPI_PLAIN / EPI_LN_FOLD, any activation; N % 128 == 0,
+// Supported: bf16 output without residual, EPI_PLAIN / EPI_LN_FOLD, any activation; or EPI_LN_STATS_HL
+// (hi/lo residual planes in and out + 64-column slab statistics: out-proj / c_proj); N % 128 == 0,
 // K % 32 == 0, K >= 64; grp == 0; no pre-activation copy.  (launch_gemm_w2b checks.)
 #include "ce_device.h"
 #include "ce_kernels.h"
@@ -85,6 +86,104 @@ __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Sum over the four 16-lane groups of a wave (lanes l, l ^ 16, l ^ 32, l ^ 48) by two lane-swap pairs
+__device__ __forceinline__ float sum_lane_groups(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// EPI_LN_STATS_HL (out-proj / c_proj of the folded towers): v = acc + bias + (hi + lo) of the residual
+// planes; hi' = bf16(v), lo' = bf16(v - hi') into the xb planes; per row the (mean, M2) of its 64
+// columns = one slab (a wave's 64 columns are exactly slab nbase / 64).  The residual of a row pair
+// (2ip, 2ip + 1) is loaded in the store layout (16 B = 8 columns of one row per lane) one pair ahead,
+// and turned into fragments by the stores' own v_permlane16_swap pairing (an involution).
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
+__device__ __forceinline__ void hl_epilogue(const GemmParams& p, const f32x4 (&acc)[8][4], const float4 (&bv)[4],
+                                            int mbase, int nbase, int rows, int fr, int fq) {
+    const int ldr = (int)p.ldr, ldo = (int)p.ldo;
+    const __amdgpu_buffer_rsrc_t hs = make_srd(p.rhl + (size_t)mbase * ldr, rows * ldr * 2);
+    const __amdgpu_buffer_rsrc_t ls = make_srd(p.rhl + p.hl_plane + (size_t)mbase * ldr, rows * ldr * 2);
+    const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
+    const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
+    const int rp = ((fr + (fq & 1) * 16) * ldr + nbase + (fq >> 1) * 8) * 2;
+    const int xp = ((fr + (fq & 1) * 16) * ldo + nbase + (fq >> 1) * 8) * 2;
+    u32x4 rh[2][4], rl[2][4];
+    auto load = [&](int ip, u32x4 (&h)[4], u32x4 (&l)[4]) __attribute__((always_inline)) {
+        int io = ip * 32 * ldr * 2;
+        asm volatile("" : "+s"(io));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            h[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(hs, rp + io + j * 32, 0, 0));
+            l[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ls, rp + io + j * 32, 0, 0));
+        }
+    };
+    float2 sta = make_float2(0.f, 0.f), stb = make_float2(0.f, 0.f);
+    load(0, rh[0], rl[0]);
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) {
+        if (ip + 1 < 4) load(ip + 1, rh[(ip + 1) & 1], rl[(ip + 1) & 1]);
+        float lmean[2], lm2[2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32x4 dh = rh[ip & 1][j], dl = rl[ip & 1][j];
+            const auto hx = __builtin_amdgcn_permlane16_swap(dh[0], dh[2], false, false);
+            const auto hy = __builtin_amdgcn_permlane16_swap(dh[1], dh[3], false, false);
+            const auto lx = __builtin_amdgcn_permlane16_swap(dl[0], dl[2], false, false);
+            const auto ly = __builtin_amdgcn_permlane16_swap(dl[1], dl[3], false, false);
+            uint2 h[2], l[2];
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const float2 a = join_hl(hx[r2], lx[r2]), b = join_hl(hy[r2], ly[r2]);
+                f32x4 v = acc[2 * ip + r2][j];
+                const float4 bb = bv[j];
+                v[0] += bb.x + a.x; v[1] += bb.y + a.y; v[2] += bb.z + b.x; v[3] += bb.w + b.y;
+                // (mean, M2) of the lane's 4 values, merged over the slab's 4 fragments (Chan)
+                const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
+                const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
+                const float q4 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
+                if (j == 0) {
+                    lmean[r2] = m4;
+                    lm2[r2] = q4;
+                } else {
+                    const float dm = m4 - lmean[r2];
+                    lmean[r2] = fmaf(dm, 1.0f / (j + 1), lmean[r2]);
+                    lm2[r2] += fmaf(dm * dm, 4.0f * j / (j + 1), q4);
+                }
+                split_hl(v[0], v[1], h[r2].x, l[r2].x);
+                split_hl(v[2], v[3], h[r2].y, l[r2].y);
+            }
+            const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
+            const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
+            const auto xx = __builtin_amdgcn_permlane16_swap(l[0].x, l[1].x, false, false);
+            const auto yy = __builtin_amdgcn_permlane16_swap(l[0].y, l[1].y, false, false);
+            const u32x4 oh = {x[0], y[0], x[1], y[1]};
+            const u32x4 ol = {xx[0], yy[0], xx[1], yy[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(oh, xs, xp + ip * 32 * ldo * 2 + j * 32, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(ol, xl, xp + ip * 32 * ldo * 2 + j * 32, 0, 0);
+        }
+        // the row's 64-column (mean, M2): the 4 lane groups' 16-value summaries combined
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2) {
+            const int i = 2 * ip + r2;
+            const float mean = sum_lane_groups(lmean[r2]) * 0.25f;
+            const float dm = lmean[r2] - mean;
+            const float q = sum_lane_groups(fmaf(dm * dm, 16.0f, lm2[r2]));
+            if (fq == (i & 3)) {
+                if (i < 4) sta = make_float2(mean, q);
+                else stb = make_float2(mean, q);
+            }
+        }
+    }
+    // lane (fr, fq) holds rows 16 fq + fr (sta) and 16 fq + fr + 64 (stb); clipped at row M
+    const int ns = p.N / 64;
+    const __amdgpu_buffer_rsrc_t ss = make_srd(p.stats_part + (size_t)mbase * ns, rows * ns * 8);
+    const int so = ((fq * 16 + fr) * ns + nbase / 64) * 8;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, sta), ss, so, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, stb), ss, so + 64 * ns * 8, 0, 0);
 }
 
 template <int ACT>
@@ -275,6 +374,10 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
     // ---- epilogue: lane holds C[mbase + 16 i + fr][nbase + 16 j + 4 fq .. +3]; rows 2ip, 2ip + 1 of a
     // lane pair (l, l ^ 16) traded by v_permlane16_swap so each lane stores 8 consecutive columns
     const int rows = max(0, min(p.M - mbase, 128));
+    if constexpr (EPI == EPI_LN_STATS_HL) {
+        hl_epilogue(p, acc, bv, mbase, nbase, rows, fr, fq);
+        return;
+    }
     const __amdgpu_buffer_rsrc_t osrd = make_srd(static_cast<bf16_t*>(p.out) + (size_t)mbase * p.ldo, rows * (int)p.ldo * 2);
     const int ldo2 = (int)p.ldo * 2;
     int voff = (fr + (fq & 1) * 16) * ldo2 + (fq >> 1) * 16 + nbase * 2;
@@ -312,13 +415,16 @@ __global__ __launch_bounds__(256, 2) void gemm_w2b(GemmParams p) {
 }  // namespace
 
 bool gemm_w2b_supported(const GemmParams& p, int epi, bool out_bf16, bool resid) {
-    return out_bf16 && !resid && (epi == EPI_PLAIN || epi == EPI_LN_FOLD) && p.N % TN == 0 && p.K % KS == 0 &&
-           p.K >= 2 * KS && p.grp == 0 && !p.m_dev && !p.pre_out && p.M > 0 &&
+    const bool base = p.N % TN == 0 && p.K % KS == 0 && p.K >= 2 * KS && p.grp == 0 && !p.m_dev && !p.pre_out &&
+                      p.M > 0;
+    if (epi == EPI_LN_STATS_HL)     // hi/lo planes in and out (the resid pointer is unused: p.rhl)
+        return base && !out_bf16 && p.rhl && p.hl_plane > 0 && p.xb && p.stats_part;
+    return base && out_bf16 && !resid && (epi == EPI_PLAIN || epi == EPI_LN_FOLD) &&
            (epi != EPI_LN_FOLD || (p.fold_c && p.fold_stats && p.bias));
 }
 
 hipError_t launch_gemm_w2b(const GemmParams& p, int act, int epi, hipStream_t s) {
-    if (!gemm_w2b_supported(p, epi, true, false)) return hipErrorInvalidValue;
+    if (!gemm_w2b_supported(p, epi, epi != EPI_LN_STATS_HL, false)) return hipErrorInvalidValue;
     const int nwg = ((p.M + TM - 1) / TM) * (p.N / TN);
     const int var = (p.variant >> 22) & 3;
 #define W2B_LAUNCH(A_, E_)                                                                                   \
@@ -328,7 +434,10 @@ hipError_t launch_gemm_w2b(const GemmParams& p, int act, int epi, hipStream_t s)
         else if (var == 3) hipLaunchKernelGGL((gemm_w2b<A_, E_, 3>), dim3(nwg), dim3(256), 0, s, p);       \
         else hipLaunchKernelGGL((gemm_w2b<A_, E_, 0>), dim3(nwg), dim3(256), 0, s, p);                     \
     } while (0)
-    if (epi == EPI_LN_FOLD) {
+    if (epi == EPI_LN_STATS_HL) {
+        if (act != ACT_NONE) return hipErrorInvalidValue;
+        W2B_LAUNCH(ACT_NONE, EPI_LN_STATS_HL);
+    } else if (epi == EPI_LN_FOLD) {
         if (act == ACT_GELU) W2B_LAUNCH(ACT_GELU, EPI_LN_FOLD);
         else if (act == ACT_QGELU) W2B_LAUNCH(ACT_QGELU, EPI_LN_FOLD);
         else W2B_LAUNCH(ACT_NONE, EPI_LN_FOLD);

@@ -129,3 +129,40 @@ def test_gemm_w2b_matches_sched11_and_is_deterministic():
     d = (outs[0] - outs[1]).abs().max().item()
     assert d <= 1e-2 * outs[0].abs().max().item(), d
     assert torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("M,N,K", [(256 * 577, 1024, 1024), (256 * 577, 1024, 4096), (1000, 768, 1024), (77, 1536, 256),
+                                   (5, 1024, 64)])
+def test_gemm_w2b_ln_stats_hl(M, N, K):
+    """The hi/lo residual-stream epilogue (epi 3: out-proj / c_proj of the folded towers) on SCHED 14:
+    resid = hi + lo planes, v = A W^T + b + resid written as planes hi = bf16(v), lo = bf16(v - hi) plus
+    per-64-column slab (mean, M2); vs torch f32 (hi + lo within 2^-16 |v| of the f32 value up to the
+    accumulation order) and rows past M untouched."""
+    g = torch.Generator(device="cpu").manual_seed(M + K + N)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    x = torch.randn(M, N, generator=g).to(DEV)
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    planes = torch.stack([hi, lo]).contiguous()
+    ref = A.float() @ W.float().t() + bias + (hi.float() + lo.float())
+    ns = N // 64
+    outp = torch.full((2, M + 64, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    part = torch.full((M + 64, ns, 2), 7.0, device=DEV)
+    # planes of M rows each: the output planes are written at xb and xb + M * N (hl_plane = M * N)
+    outv = outp.view(-1)[: 2 * M * N].view(2, M, N)
+    cnt = run14(lambda: _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), None,
+                                  _lib.CE_F32, 3, P(outv), P(part), None, None))
+    assert cnt[W2 + 1] == 1, cnt
+    scale = ref.abs().max().item()
+    v = outv[0].float() + outv[1].float()
+    assert (v - ref).abs().max().item() <= 2e-4 * scale + 1e-5
+    assert (outv[0].float() - v).abs().max().item() <= 2 ** -8 * scale
+    assert bool((outp.view(-1)[2 * M * N:] == 7.0).all())
+    r3 = ref.reshape(M, ns, 64)
+    mean = r3.mean(-1)
+    m2 = ((r3 - mean[..., None]) ** 2).sum(-1)
+    assert (part[:M, :, 0] - mean).abs().max().item() <= 1e-4 * scale
+    assert (part[:M, :, 1] - m2).abs().max().item() <= 1e-4 * m2.abs().max().item() + 1e-4
+    assert bool((part[M:] == 7.0).all())
