@@ -600,8 +600,172 @@ __global__ __launch_bounds__(256, 2) void attn_bwd2_k(bf16_t* __restrict__ dqkv,
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Attention backward, v3 (default; ce_set_attn_bwd_variant(2) keeps v2): v2's arithmetic with
+//  * the causal structure used: phase 1 runs only the score tiles on or below the diagonal (15 of 25
+//    at L = 77), and each phase-2 product contracts only over the blocks that can be non-zero — dq'
+//    row block ti over key blocks 0..ti, dk / dv key block tj over query blocks tj..nt-1 (180 instead
+//    of 300 16-deep MFMA steps at L = 77); every skipped product term is an exact zero (P = dS = 0
+//    above the diagonal), so the sums are v2's up to the MFMA step split;
+//  * all 15 row loads of a thread issued before the first use (v2 waits per 5);
+//  * the outputs staged in LDS and written as whole 128-B rows (16 B per lane) instead of 2-byte
+//    stores of 4 rows x 32 B per wave instruction.
+template <bool XT, bool YT>
+__device__ __forceinline__ f32x4 mfma_tile3(const bf16_t* X, int ldx, const bf16_t* Y, int ldy, int m0, int n0, int k0,
+                                            int k1, int lane) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (; k0 + 32 <= k1; k0 += 32)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag8<XT>(X, ldx, m0, k0, lane), frag8<YT>(Y, ldy, n0, k0, lane),
+                                                      acc, 0, 0, 0);
+    if (k0 < k1)
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(frag4<XT>(X, ldx, m0, k0, lane), frag4<YT>(Y, ldy, n0, k0, lane),
+                                                        acc, 0, 0, 0);
+    return acc;
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd3_k(bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ qkv,
+                                                      const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                      const float* __restrict__ lse, int L, int H, int causal,
+                                                      float* __restrict__ bpart) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);            // [80][AB_LD]
+    bf16_t* Ks = Qs + AB_L * AB_LD;
+    bf16_t* Vs = Ks + AB_L * AB_LD;
+    bf16_t* dOs = Vs + AB_L * AB_LD;
+    bf16_t* Ps = dOs + AB_L * AB_LD;                         // [80][AB2_LP]  P[i][j]
+    bf16_t* dSs = Ps + AB_L * AB2_LP;                        // [80][AB2_LP]  dS[i][j]
+    float* delta = reinterpret_cast<float*>(dSs + AB_L * AB2_LP);   // [80]
+    float* lrow = delta + AB_L;                                      // [80]
+    bf16_t* Out = Qs;                                        // [3][80][64], after phase 2
+
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int D = H * 64, ld = 3 * D;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nt = (L + 15) / 16, K = nt * 16;
+    if (tid < AB_L) lrow[tid] = tid < L ? lse[(size_t)bh * L + tid] : 0.f;
+    // q', k, v, dO rows (zero past L) + delta_i = dO_i . O_i; the 3 chunks of a thread loaded first
+    {
+        uint4 q[3], k[3], v[3], g[3], o[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int e = tid + 256 * u, i = e >> 3, c = (e & 7) * 8;
+            q[u] = k[u] = v[u] = g[u] = o[u] = make_uint4(0, 0, 0, 0);
+            if (e < AB_L * 8 && i < L) {
+                const size_t row = (size_t)(b * L + i);
+                q[u] = *reinterpret_cast<const uint4*>(qkv + row * ld + h * 64 + c);
+                k[u] = *reinterpret_cast<const uint4*>(qkv + row * ld + D + h * 64 + c);
+                v[u] = *reinterpret_cast<const uint4*>(qkv + row * ld + 2 * D + h * 64 + c);
+                g[u] = *reinterpret_cast<const uint4*>(dO + row * D + h * 64 + c);
+                o[u] = *reinterpret_cast<const uint4*>(O + row * D + h * 64 + c);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int e = tid + 256 * u, i = e >> 3, c = (e & 7) * 8;
+            if (e >= AB_L * 8) break;       // (u = 2: lanes 128..255 of the block, whole waves)
+            *reinterpret_cast<uint4*>(Qs + i * AB_LD + c) = q[u];
+            *reinterpret_cast<uint4*>(Ks + i * AB_LD + c) = k[u];
+            *reinterpret_cast<uint4*>(Vs + i * AB_LD + c) = v[u];
+            *reinterpret_cast<uint4*>(dOs + i * AB_LD + c) = g[u];
+            const bf16_t* gs = reinterpret_cast<const bf16_t*>(&g[u]);
+            const bf16_t* os = reinterpret_cast<const bf16_t*>(&o[u]);
+            float part = 0.f;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) part += bf2f(gs[t]) * bf2f(os[t]);
+            part += __shfl_xor(part, 1, 64);
+            part += __shfl_xor(part, 2, 64);
+            part += __shfl_xor(part, 4, 64);
+            if ((e & 7) == 0) delta[i] = part;
+        }
+    }
+    __syncthreads();
+    // phase 1: S = q' k^T -> P = exp2(S - lse) (masked) -> dP = dO V^T -> dS, for the score tiles that
+    // hold an unmasked entry (causal: tj <= ti; t enumerates the lower triangle row by row)
+    const int ntile = causal ? nt * (nt + 1) / 2 : nt * nt;
+    for (int t = wave; t < ntile; t += 4) {
+        int ti, tj;
+        if (causal) {
+            ti = 0;
+            while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+            tj = t - ti * (ti + 1) / 2;
+        } else {
+            ti = t / nt;
+            tj = t - ti * nt;
+        }
+        const f32x4 sv = mfma_tile3<false, false>(Qs, AB_LD, Ks, AB_LD, ti * 16, tj * 16, 0, 64, lane);
+        const f32x4 dp = mfma_tile3<false, false>(dOs, AB_LD, Vs, AB_LD, ti * 16, tj * 16, 0, 64, lane);
+        const int j = tj * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = ti * 16 + 4 * (lane >> 4) + q;
+            const bool ok = i < L && j < L && !(causal && j > i);
+            const float p = ok ? exp2f(sv[q] - lrow[i]) : 0.f;
+            const float ds = ok ? 0.69314718055994531f * p * (dp[q] - delta[i]) : 0.f;
+            Ps[i * AB2_LP + j] = f2bf(p);
+            dSs[i * AB2_LP + j] = f2bf(ds);
+        }
+    }
+    __syncthreads();
+    // phase 2: dq'[i][d] = sum_j dS[i][j] k[j][d];  dk[j][d] = sum_i dS[i][j] q'[i][d];  dv[j][d] = sum_i
+    // P[i][j] dO[i][d].  Wave w owns column block w of every product (fixed-order column sums for bpart);
+    // results stay in registers (bf16 pairs) until every wave's LDS reads are done
+    uint2 res[3][AB_L / 16];
+    float csum[3] = {0.f, 0.f, 0.f};
+    const int n0 = wave * 16;
+#pragma unroll
+    for (int which = 0; which < 3; ++which)
+#pragma unroll
+        for (int ti = 0; ti < AB_L / 16; ++ti) {
+            res[which][ti] = make_uint2(0, 0);
+            if (ti >= nt) continue;
+            const int m0 = ti * 16;
+            f32x4 r;
+            if (which == 0) r = mfma_tile3<false, true>(dSs, AB2_LP, Ks, AB_LD, m0, n0, 0, causal ? m0 + 16 : K, lane);
+            else if (which == 1) r = mfma_tile3<true, true>(dSs, AB2_LP, Qs, AB_LD, m0, n0, causal ? m0 : 0, K, lane);
+            else r = mfma_tile3<true, true>(Ps, AB2_LP, dOs, AB_LD, m0, n0, causal ? m0 : 0, K, lane);
+            const uint32_t p01 = pack_bf2(r[0], r[1]), p23 = pack_bf2(r[2], r[3]);
+            res[which][ti] = make_uint2(p01, p23);
+            // column sums of the bf16-rounded values of rows < L (the in_proj bias gradient)
+            const int i0 = m0 + 4 * (lane >> 4);
+            const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
+            const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
+            csum[which] += (i0 < L ? v0 : 0.f) + (i0 + 1 < L ? v1 : 0.f) + (i0 + 2 < L ? v2 : 0.f) +
+                           (i0 + 3 < L ? v3 : 0.f);
+        }
+    if (bpart) {
+#pragma unroll
+        for (int which = 0; which < 3; ++which) {
+            float c = csum[which];
+            c += __shfl_xor(c, 16, 64);
+            c += __shfl_xor(c, 32, 64);
+            if (lane < 16) bpart[(size_t)b * 3 * D + which * D + h * 64 + n0 + lane] = c;
+        }
+    }
+    __syncthreads();
+    // stage the three [L][64] outputs in LDS, then write whole 128-B rows
+#pragma unroll
+    for (int which = 0; which < 3; ++which)
+#pragma unroll
+        for (int ti = 0; ti < AB_L / 16; ++ti) {
+            if (ti >= nt) continue;
+            const int i0 = ti * 16 + 4 * (lane >> 4), col = n0 + (lane & 15);
+            bf16_t* op = Out + ((size_t)which * AB_L + i0) * 64 + col;
+            const uint2 w = res[which][ti];
+            op[0] = (bf16_t)(w.x & 0xffffu);
+            op[64] = (bf16_t)(w.x >> 16);
+            op[128] = (bf16_t)(w.y & 0xffffu);
+            op[192] = (bf16_t)(w.y >> 16);
+        }
+    __syncthreads();
+    for (int e = tid; e < 3 * L * 8; e += 256) {
+        const int which = e / (L * 8), rem = e - which * L * 8, i = rem >> 3, c = (rem & 7) * 8;
+        *reinterpret_cast<uint4*>(dqkv + (size_t)(b * L + i) * ld + which * D + h * 64 + c) =
+            *reinterpret_cast<const uint4*>(Out + ((size_t)which * AB_L + i) * 64 + c);
+    }
+}
+
 std::atomic<int> g_attn_bwd_var{kKnobUnset};     // A/B knob (knobs.h)
-int attn_bwd_env() { return env_int("CE_ATTN_BWD", 2) == 1 ? 1 : 2; }
+int attn_bwd_env() { const int v = env_int("CE_ATTN_BWD", 3); return v == 1 || v == 2 ? v : 3; }
 int attn_bwd_variant() { return knob_get(g_attn_bwd_var, attn_bwd_env); }
 
 // ---------------------------------------------------------------------------------------------
@@ -931,14 +1095,21 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
         (void)hipFuncSetAttribute((const void*)attn_bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAttnBwdLds);
         attr[dev].store(true, std::memory_order_release);
     }
-    if (attn_bwd_variant() == 2) {
+    const int var = attn_bwd_variant();
+    if (var >= 2) {
         if (!attr2[dev].load(std::memory_order_acquire)) {
             (void)hipFuncSetAttribute((const void*)attn_bwd2_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kAttnBwd2Lds);
+            (void)hipFuncSetAttribute((const void*)attn_bwd3_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kAttnBwd2Lds);
             attr2[dev].store(true, std::memory_order_release);
         }
-        hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse, L,
-                           H, causal ? 1 : 0, dbias ? bpart : nullptr);
+        if (var == 3)
+            hipLaunchKernelGGL(attn_bwd3_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse,
+                               L, H, causal ? 1 : 0, dbias ? bpart : nullptr);
+        else
+            hipLaunchKernelGGL(attn_bwd2_k, dim3((unsigned)(B * H)), dim3(256), kAttnBwd2Lds, s, dqkv, qkv, O, dO, lse,
+                               L, H, causal ? 1 : 0, dbias ? bpart : nullptr);
         if (dbias)   // in_proj bias gradient: the captions' column sums (two-stage, fixed order)
             return launch_colsum(dbias, bpart, true, 3 * H * 64, B, 3 * H * 64, 1.0f, false, scratch, s);
         return hipGetLastError();
@@ -951,7 +1122,7 @@ hipError_t launch_attention_bwd(bf16_t* dqkv, const bf16_t* qkv, const bf16_t* O
 
 int set_attn_bwd_variant(int v) {
     const int prev = attn_bwd_variant();
-    g_attn_bwd_var.store(v == 1 ? 1 : 2);
+    g_attn_bwd_var.store(v == 1 || v == 2 ? v : 3);
     return prev;
 }
 

@@ -324,10 +324,12 @@ int ce_set_gemm_variant(int bits);
  * default (381 = 125 + 256).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
-/* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 2 = the
- * transposed-read kernel (default: operands contracted over their image's row index come from
- * ds_read_b64_tr_b16, 73 KB of LDS, two workgroups per CU), 1 = the kernel with transposed LDS copies
- * (136 KB, one per CU).  Returns the previous setting. */
+/* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 3 = the
+ * default: the transposed-read kernel with the causal structure used (only the score tiles on or below
+ * the diagonal, contractions over the blocks that can be non-zero) and the outputs written as whole
+ * rows from LDS; 2 = the transposed-read kernel over every tile (operands contracted over their image's
+ * row index come from ds_read_b64_tr_b16, 73 KB of LDS, two workgroups per CU); 1 = the kernel with
+ * transposed LDS copies (136 KB, one per CU).  Returns the previous setting. */
 int ce_set_attn_bwd_variant(int v);
 /* Weight-gradient GEMM with MN-major operands: C[m][n] = scale_m * sum_k A[k][m] B[k][n]
  * with A [K][lda], B [K][ldb] bf16 row-major (the activations of a linear layer's input and output

@@ -119,3 +119,40 @@ def test_text_forward_overlap_is_bitwise_neutral(golden):
         out[overlap] = (float(loss), tr.grad.clone())
     assert out[True][0] == out[False][0]
     assert torch.equal(out[True][1], out[False][1])
+
+
+def test_attention_backward_variants_agree(golden):
+    """The three attention-backward kernels (3: causal-block skipping + staged row stores, the default;
+    2: transposed reads; 1: transposed LDS copies) compute the same sums — the skipped terms are exact
+    zeros — so the whole step's gradient agrees to f32 rounding of the MFMA step split."""
+    from clipembed import _lib
+    g = golden("train")
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 2)
+    m = clipembed.CLIP(cfg)
+    m.load_state_dict(W.synthetic_state_dict(cfg))
+    m.to("cuda")
+    tr = TextTowerTrainer(m, lr=LR, weight_decay=WD, usehardtext=True)
+    imgs = torch.from_numpy(W.synthetic_images(4, seed=int(g["images_seed"]))).cuda()
+    caps = torch.from_numpy(g["captions"]).cuda()
+    L = _lib.lib()
+    out = {}
+    prev = L.ce_set_attn_bwd_variant(3)
+    try:
+        for v in (3, 2, 1):
+            L.ce_set_attn_bwd_variant(v)
+            loss = tr.compute_grads(imgs, caps)
+            torch.cuda.synchronize()
+            out[v] = (float(loss), tr.grad.clone())
+    finally:
+        L.ce_set_attn_bwd_variant(prev)
+    assert prev == 3                                   # the default
+    for v in (2, 1):
+        assert out[v][0] == out[3][0]                  # the forward is unchanged
+        d = (out[v][1] - out[3][1]).abs().max().item()
+        assert d <= 1e-3 * out[3][1].abs().max().item(), (v, d)
+        for n, gv in tr.gviews.items():
+            off = (gv.data_ptr() - tr.grad.data_ptr()) // 4
+            a = out[3][1][off:off + gv.numel()].double()
+            b = out[v][1][off:off + gv.numel()].double()
+            c = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+            assert c > 0.99999 or a.norm() < 1e-12, (v, n, c)
