@@ -21,6 +21,7 @@
 //  * K tile LDS image swizzled (16-B chunk c of row r at c ^ ((r>>1)&7)) for conflict-free
 //    ds_read_b128; ragged tails (L = 577 = 9*64 + 1, L = 77) are clamped on load and masked
 //    with -inf in the scores.
+#include <cstdio>
 #include <type_traits>
 
 #include "ce_device.h"
@@ -29,6 +30,8 @@
 
 namespace ce {
 namespace {
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
 constexpr int QBLK = 128;
 constexpr int KBLK = 64;
@@ -233,8 +236,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+            // v_dot2_f32_bf16 on the bf16 pairs: 16 instructions instead of 32 FMAs + 64 unpacks
 #pragma unroll
-            for (int e = 0; e < 8; ++e) a = fmaf((float)qf[ks][e], (float)kv[e], a);
+            for (int e = 0; e < 4; ++e) {
+                const bf16x2_t qa = {qf[ks][2 * e], qf[ks][2 * e + 1]};
+                const bf16x2_t ka = {kv[2 * e], kv[2 * e + 1]};
+                a = __builtin_amdgcn_fdot2_f32_bf16(qa, ka, a, false);
+            }
         }
         s0v = a + __shfl_xor(a, 32, 64);
         fix_ok = MODE >= 1 && __all(s0v <= 64.0f && s0v >= -64.0f);
@@ -248,10 +256,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
-                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
-                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
-                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
-                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
+                const f32x2 pp = {p0, p0};
+                const f32x2 x0 = f32x2{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u)} * pp;
+                const f32x2 x1 = f32x2{__uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)} * pp;
+                o[dt][4 * g + 0] = x0.x; o[dt][4 * g + 1] = x0.y;
+                o[dt][4 * g + 2] = x1.x; o[dt][4 * g + 3] = x1.y;
             }
     }
 
@@ -542,10 +551,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
             for (int gp = 0; gp < 2; ++gp) {
                 const int g0 = 2 * gp, g1 = 2 * gp + 1;
-                const uint32_t ax = pack_bf2(o[dt][4 * g0 + 0] * inv, o[dt][4 * g0 + 1] * inv);
-                const uint32_t ay = pack_bf2(o[dt][4 * g0 + 2] * inv, o[dt][4 * g0 + 3] * inv);
-                const uint32_t bx = pack_bf2(o[dt][4 * g1 + 0] * inv, o[dt][4 * g1 + 1] * inv);
-                const uint32_t by = pack_bf2(o[dt][4 * g1 + 2] * inv, o[dt][4 * g1 + 3] * inv);
+                // (v_pk_mul_f32: no MFMAs to sit beside here)
+                const f32x2 iv = {inv, inv};
+                const f32x2 a0 = f32x2{o[dt][4 * g0 + 0], o[dt][4 * g0 + 1]} * iv;
+                const f32x2 a1 = f32x2{o[dt][4 * g0 + 2], o[dt][4 * g0 + 3]} * iv;
+                const f32x2 b0 = f32x2{o[dt][4 * g1 + 0], o[dt][4 * g1 + 1]} * iv;
+                const f32x2 b1 = f32x2{o[dt][4 * g1 + 2], o[dt][4 * g1 + 3]} * iv;
+                const uint32_t ax = pack_bf2(a0.x, a0.y), ay = pack_bf2(a1.x, a1.y);
+                const uint32_t bx = pack_bf2(b0.x, b0.y), by = pack_bf2(b1.x, b1.y);
                 const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
                 const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
                 if (qrow < L)
@@ -562,6 +575,376 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 w.y = pack_bf2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
                 *reinterpret_cast<uint2*>(op + d0) = w;
             }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent vision-tower variant (knob 893 = 381 | 512, selectable where 381 applies and no lse /
+// packed sequences are asked for; measured slower than 381): the 381 feature set (fixed-offset softmax, key 0 up front, one
+// barrier per key tile, asm V^T reads, 16-B stores, buffer-descriptor DMAs) on a grid of resident
+// workgroups walking the q-blocks in rounds.  The next block's Q rows, key-0 rows and
+// first K/V tile are LDS-DMA'd during the current block's last key tile, so a block starts on data
+// already in LDS: at L = 577 a q-block runs only 9 key tiles, and the start-up of a freshly
+// dispatched workgroup (Q and key 0 from HBM, tile 0's DMA, nothing to overlap with) had cost about
+// three tiles' worth per block (tools/bench_kernels.py: 788 TF/s at L = 577 against 1017 at L = 2305,
+// same FLOPs).  LDS: the K/V ring (2 x 16 KB), the Q image (128 rows x 128 B, 16-B chunk c of row r at
+// c ^ (r & 7): conflict-free ds_read_b128 of 8 rows), key 0's K and V rows (one DMA, 1 KB written).
+template <int VAR>
+__global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                     int L, int H, int nblk, float qscale) {
+    constexpr int QOFF = 2 * STAGE_BYTES;
+    constexpr int COFF = QOFF + QBLK * 128;
+    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024];
+    // blocks slot, slot + G, slot + 2G, ...: the grid walks the blocks in rounds, and slot is the XCD-aware
+    // remap of attn_fwd, so the q-blocks of one (batch, head) run at the same time on one XCD and
+    // share its K / V tiles in that XCD's L2 (contiguous runs per workgroup re-read every head's K / V
+    // from HBM once per q-block: 649 against 711 TF/s at L = 577, profiles/r05/r05j_*, r05k_*)
+    const int G = gridDim.x;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qn = G >> 3, rn = G & 7;
+    const int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    if (blk_first >= nblk) return;        // workgroup-uniform
+    const int nqb = (L + QBLK - 1) / QBLK;
+    const int D = H * 64;
+    const int ld2 = 6 * D;                // bytes per qkv row
+    const int Lk = L - 1;                 // keys 1 .. L - 1 fill the tiles (launcher: Lk % 64 == 0)
+    const int nkt = Lk / KBLK;
+    const int nrec = (Lk - 1) * ld2 + 128;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h2 = lane >> 5;
+    // K/V staging (as attn_fwd): thread -> row tid >> 3 of a 32-row pass, 16-B chunk tid & 7
+    const int srow = tid >> 3;
+    const int spos = tid & 7;
+    const int kchunk = spos ^ ((tid >> 4) & 7);
+    const int vchunk = spos ^ (((srow >> 1) & 1) << 2);
+    int kvo[2], vvo[2];
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+        kvo[ps] = (ps * 32 + srow) * ld2 + kchunk * 16;
+        vvo[ps] = (ps * 32 + srow) * ld2 + vchunk * 16;
+    }
+    int koff[2][4];
+#pragma unroll
+    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int row = kt2 * 32 + r;
+            koff[kt2][ks] = row * 128 + (((2 * ks + h2) ^ ((row >> 1) & 7)) << 4);
+        }
+    const int Gq = lane >> 4, gi = lane & 15;
+    const int vq = gi >> 2, vp = gi & 3;
+    unsigned vaddr[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+        const int chunk = dt * 4 + 2 * (Gq & 1) + (vp >> 1);
+        const int voff = (4 * (Gq >> 1) + vq) * 128 + ((chunk ^ (((vq >> 1) & 1) << 2)) << 4) + (vp & 1) * 8;
+        vaddr[dt] = (unsigned)(uintptr_t)(CE_LDS void*)(smem + voff);
+    }
+    // Q image reads: row wave * 32 + r ((wave * 32 + r) & 7 = r & 7), 16-B chunk 2 ks + h2
+    int qoff[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qoff[ks] = QOFF + (wave * 32 + r) * 128 + (((2 * ks + h2) ^ (r & 7)) << 4);
+    // Q staging: wave w's 32 rows, 8 per DMA; lane -> row lane >> 3 of the 8, chunk (lane & 7) ^ (lane >> 3)
+    const int qchunk = (lane & 7) ^ (lane >> 3);
+
+    // block -> (batch, head, q-block); hb = byte address of row 0 of the sequence, column h * 64 (q third)
+    struct Blk {
+        int qb;
+        long orow0;                       // first output row of the sequence
+        int ocol;
+        const char* hb;
+    };
+    auto decode = [&](int bk) {
+        Blk k;
+        const int bh = bk / nqb;
+        k.qb = bk - bh * nqb;
+        const int b = bh / H, h = bh - b * H;
+        k.orow0 = (long)b * L;
+        k.ocol = h * 64;
+        k.hb = reinterpret_cast<const char*>(qkv) + (size_t)b * L * ld2 + h * 128;
+        return k;
+    };
+    auto stage_kv = [&](int t, auto bufc, __amdgpu_buffer_rsrc_t ks_, __amdgpu_buffer_rsrc_t vs_) {
+        constexpr int BUF = decltype(bufc)::value;
+        char* dst = smem + BUF * STAGE_BYTES + wave * 1024;
+        const int ro = t * KBLK * ld2;
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            // (the tile's row offset as the scalar offset: no per-tile VGPR offsets for hipcc to hoist)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ks_, (CE_LDS void*)(dst + ps * 4096), 16, kvo[ps], ro, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(vs_, (CE_LDS void*)(dst + TILE_KV_BYTES + ps * 4096), 16,
+                                                     vvo[ps], ro, 0, 0);
+        }
+    };
+    // Q rows (clamped to L - 1: the lanes past the end compute row L - 1's values again) and key 0's
+    // K / V rows (wave 0: lanes 0-7 K, 8-15 V, the rest repeat them into the area's unused bytes)
+    auto stage_q = [&](int qb, __amdgpu_buffer_rsrc_t qs_) {
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) {
+            const int row = min(qb * QBLK + wave * 32 + ps * 8 + (lane >> 3), L - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qs_, (CE_LDS void*)(smem + QOFF + wave * 4096 + ps * 1024), 16,
+                                                     row * ld2 + qchunk * 16, 0, 0, 0);
+        }
+        if (wave == 0) {
+            const int i = lane & 15;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(qs_, (CE_LDS void*)(smem + COFF), 16,
+                                                     (i < 8 ? 2 * D : 4 * D) + (i & 7) * 16, 0, 0, 0);
+        }
+    };
+
+    Blk cur = decode(blk_first);
+    __amdgpu_buffer_rsrc_t qsrd = attn_srd(cur.hb, (L - 1) * ld2 + 128);
+    __amdgpu_buffer_rsrc_t ksrd = attn_srd(cur.hb + 2 * D + ld2, nrec);
+    __amdgpu_buffer_rsrc_t vsrd = attn_srd(cur.hb + 4 * D + ld2, nrec);
+    stage_q(cur.qb, qsrd);
+    stage_kv(0, std::integral_constant<int, 0>{}, ksrd, vsrd);
+    int par = 0;                          // ring slot of the block's tile 0
+    bool stores_out = false;              // the previous block's 4 output stores may be in flight
+    const f32x16 zero16 = {};
+
+    for (int blk = blk_first; blk < nblk; blk += G) {
+        // this block's Q, key-0 rows and K/V tile 0 landed (counted: the 4 stores after them may not)
+        if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier();
+        const bool has_next = blk + G < nblk;
+        const Blk nxt = decode(has_next ? blk + G : blk);
+        const __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
+        const __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
+        const __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
+        const int q_wave0 = cur.qb * QBLK + wave * 32;
+        const int qrow = q_wave0 + r;
+        const bool active = q_wave0 < L;  // wave-uniform
+
+        bf16x8 qf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(smem + qoff[ks]);
+        if (qscale != 1.0f) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
+        }
+        // key 0: its score (v_dot2_f32_bf16 on the bf16 pairs, both lane halves summed) and its term in O / l
+        f32x16 o[2];
+        float m_run = 0.f, l_run = 0.f;
+        float s0v;
+        {
+            float a = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const bf16x8 kv = *reinterpret_cast<const bf16x8*>(smem + COFF + (2 * ks + h2) * 16);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const bf16x2_t qa = {qf[ks][2 * e], qf[ks][2 * e + 1]};
+                    const bf16x2_t ka = {kv[2 * e], kv[2 * e + 1]};
+                    a = __builtin_amdgcn_fdot2_f32_bf16(qa, ka, a, false);
+                }
+            }
+            s0v = a + __shfl_xor(a, 32, 64);
+        }
+        const bool fix_ok = __all(s0v <= 64.0f && s0v >= -64.0f);
+        bool fast = fix_ok;
+        float p0 = 1.0f;
+        if (fix_ok) p0 = __builtin_amdgcn_exp2f(s0v);
+        else m_run = s0v;
+        if (h2 == 0) l_run = p0;
+        // (key 0's V row by inline asm: the compiler would wait vmcnt(0) before a plain LDS read here, for
+        // the previous block's output stores)
+        uint2 v0w[2][4];
+        {
+            const unsigned va = (unsigned)(uintptr_t)(CE_LDS void*)(smem + COFF + 128 + 8 * h2);
+#define CE_V0(DT, G) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v0w[DT][G]) : "v"(va), "n"(((DT) * 32 + 8 * (G)) * 2))
+            CE_V0(0, 0); CE_V0(0, 1); CE_V0(0, 2); CE_V0(0, 3);
+            CE_V0(1, 0); CE_V0(1, 1); CE_V0(1, 2); CE_V0(1, 3);
+#undef CE_V0
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint2 w = v0w[dt][g];
+                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
+                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
+                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
+                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
+            }
+
+        auto pv_asm = [&](auto vbc, const bf16x8 (&pf)[2][2]) {
+            constexpr int VB = decltype(vbc)::value;
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            s16x4 vr[2][2][2];
+#define CE_TRV(R, DT, H, OFF) \
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[R][DT][H]) : "v"(vaddr[DT]), "n"(OFF))
+#define CE_ISSUE(Q) \
+    CE_TRV((Q) & 1, 0, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
+    CE_TRV((Q) & 1, 0, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024); \
+    CE_TRV((Q) & 1, 1, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
+    CE_TRV((Q) & 1, 1, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024)
+            auto mf = [&](int q) {
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[q >> 1][q & 1],
+                                                                   o[dt], 0, 0, 0);
+                }
+            };
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q == 0) { CE_ISSUE(0); }
+                else if (q == 1) { CE_ISSUE(1); }
+                else if (q == 2) { CE_ISSUE(2); }
+                else { CE_ISSUE(3); }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                mf(q);
+            }
+#undef CE_ISSUE
+#undef CE_TRV
+        };
+        auto rescale = [&](float delta) {
+            const float alpha = __builtin_amdgcn_exp2f(-delta);
+            l_run *= alpha;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+            m_run += delta;
+        };
+        auto tile = [&](const int t, auto bufc) {
+            constexpr int BUF = decltype(bufc)::value;
+            // tile t landed and every wave is done with tile t - 1 (tile 0: the block-start barrier; with a
+            // single tile, the Q / key-0 reads before the next block's DMAs overwrite them)
+            if (t > 0 || nkt == 1) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                barrier();
+            }
+            if (t + 1 < nkt) {
+                stage_kv(t + 1, std::integral_constant<int, BUF ^ 1>{}, ksrd, vsrd);
+            } else if (has_next) {
+                stage_kv(0, std::integral_constant<int, BUF ^ 1>{}, nksrd, nvsrd);
+                stage_q(nxt.qb, nqsrd);
+            }
+            const char* kb = smem + BUF * STAGE_BYTES;
+            bool redo = false;
+            const bool fast_tile = fast;   // wave-uniform
+            if (active && fast_tile) {
+                f32x16 s[2];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int ks = 0; ks < 4; ++ks) {
+                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                        s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? zero16 : s[kt2], 0, 0, 0);
+                    }
+                float ps[4] = {0.f, 0.f, 0.f, 0.f};
+                bf16x8 pf[2][2];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                            ps[j & 3] += pv_;
+                            pf[kt2][s2][j] = (__bf16)pv_;
+                        }
+                const float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+                const bool overflow = __any(!(psum <= 0x1p64f)) || (t == 0 && __any(!(psum >= 0x1p-64f)));
+                if (!overflow) {
+                    l_run += psum;
+                    __builtin_amdgcn_sched_barrier(0);
+                    pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
+                } else {
+                    fast = false;
+                    redo = true;
+                }
+            }
+            if (active && (redo || !fast_tile)) {
+                // general online softmax (rare: a row max outside +-64 in log2 units)
+                f32x16 s[2];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) s[kt2][i] = -m_run;
+#pragma unroll
+                    for (int ks = 0; ks < 4; ++ks) {
+                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                        s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
+                    }
+                }
+                float tmax = s[0][0];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax = fmaxf(tmax, s[kt2][i]);
+                tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+                const bool fix0 = t == 0 && fix_ok && __all(tmax <= 64.0f && tmax >= -64.0f);
+                if (fix0) fast = true;
+                if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
+                    const float delta = t == 0 ? fmaxf(tmax, s0v - m_run) : fmaxf(tmax, 0.f);
+                    rescale(delta);
+                    fast = false;
+#pragma unroll
+                    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) s[kt2][i] -= delta;
+                }
+                float psum = 0.f;
+                bf16x8 pf[2][2];
+#pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                            psum += pv_;
+                            pf[kt2][s2][j] = (__bf16)pv_;
+                        }
+                l_run += psum;
+                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
+            }
+        };
+        auto run = [&](auto pc) {
+            constexpr int P = decltype(pc)::value;
+            for (int t = 0; t < nkt; t += 2) {
+                tile(t, std::integral_constant<int, P>{});
+                if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, P ^ 1>{});
+            }
+        };
+        if (par) run(std::integral_constant<int, 1>{});
+        else run(std::integral_constant<int, 0>{});
+
+        // epilogue: O = O^T / l, 16-B stores (lanes l, l^32 trade halves); rows past L repeat row L - 1
+        if (active) {
+            const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+            const float inv = 1.0f / l_tot;
+            bf16_t* op = out + (size_t)(cur.orow0 + min(qrow, L - 1)) * D + cur.ocol;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int gp = 0; gp < 2; ++gp) {
+                    const int g0 = 2 * gp, g1 = 2 * gp + 1;
+                    const f32x2 iv = {inv, inv};
+                    const f32x2 a0 = f32x2{o[dt][4 * g0 + 0], o[dt][4 * g0 + 1]} * iv;
+                    const f32x2 a1 = f32x2{o[dt][4 * g0 + 2], o[dt][4 * g0 + 3]} * iv;
+                    const f32x2 b0 = f32x2{o[dt][4 * g1 + 0], o[dt][4 * g1 + 1]} * iv;
+                    const f32x2 b1 = f32x2{o[dt][4 * g1 + 2], o[dt][4 * g1 + 3]} * iv;
+                    const uint32_t ax = pack_bf2(a0.x, a0.y), ay = pack_bf2(a1.x, a1.y);
+                    const uint32_t bx = pack_bf2(b0.x, b0.y), by = pack_bf2(b1.x, b1.y);
+                    const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                    const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                    *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
+                }
+        }
+        stores_out = active;
+        cur = nxt;
+        qsrd = nqsrd; ksrd = nksrd; vsrd = nvsrd;
+        par ^= nkt & 1;
     }
 }
 
@@ -714,6 +1097,29 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 #define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
+    const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
+    if (!causal && v == 893 && clsk_ok && !lse && !seg) {
+        // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
+        static std::atomic<int> occ[kMaxDevices];
+        const int dev = current_device();
+        int per_cu = occ[dev].load(std::memory_order_acquire);
+        if (per_cu <= 0) {
+            int q = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, reinterpret_cast<const void*>(attn_fwd_p<893>), 256, 0) !=
+                    hipSuccess || q <= 0)
+                q = 2;
+            const int ov = env_int("CE_ATTN_PERSIST_OCC", 0);      // A/B: workgroups per CU
+            if (env_int("CE_ATTN_DEBUG", 0)) fprintf(stderr, "attn_fwd_p: occupancy %d per CU, override %d\n", q, ov);
+            if (ov > 0) q = ov;
+            occ[dev].store(q, std::memory_order_release);
+            per_cu = q;
+        }
+        const long nblk = (long)((L + QBLK - 1) / QBLK) * H * B;
+        if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
+        const int g = (int)std::min<long>(nblk, (long)per_cu * device_cus());
+        hipLaunchKernelGGL((attn_fwd_p<893>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
+        return hipGetLastError();
+    }
     if (causal) {
         if ((v & 88) == 88) CE_ATTN_LAUNCH(true, 88);
         else if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
@@ -721,7 +1127,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v & 256) && !((L - 1) % KBLK == 0 && L > 1) ? (v & ~256) : v;
+        const int vv = v == 893 ? (clsk_ok ? 381 : 125) : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
             case 381: CE_ATTN_LAUNCH(false, 381); break;
             case 125: CE_ATTN_LAUNCH(false, 125); break;
@@ -748,7 +1154,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61 || var == 125 || var == 253 || var == 381)
+                  var == 61 || var == 125 || var == 253 || var == 381 || var == 893)
                      ? var : 381;
     return prev;
 }

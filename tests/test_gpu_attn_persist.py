@@ -1,0 +1,55 @@
+"""Attention variant 893 (csrc/attention.hip attn_fwd_p): the 381 feature set on a grid of resident
+workgroups, walking the q-blocks in rounds with the next block's Q rows, key-0 rows and
+first K/V tile DMA'd during the current block's last key tile.  Checked against the torch f32
+reference and variant 381 on grids of several blocks per workgroup (so both ring parities of odd
+tile counts, the block seams and the prefetch run), single-tile blocks (L = 65: the next block's
+DMAs follow that tile's own barrier), the image tower's L = 577 with its one-row last q-block, a
+dominant late key (the fast tile's overflow check sends the wave to the general path mid-block) and
+run-to-run bitwise determinism."""
+import pytest
+import torch
+
+from clipembed import _lib
+from test_gpu_kernels import attn_ref, run_attn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def run_var(var, qkv, B, L, H):
+    L_ = _lib.lib()
+    prev = L_.ce_set_attn_variant(var)
+    try:
+        return run_attn(qkv, B, L, H, False).float()
+    finally:
+        L_.ce_set_attn_variant(prev)
+
+
+@pytest.mark.parametrize("B,L,H,scale", [(32, 577, 16, 1.0), (64, 65, 16, 1.0), (40, 129, 16, 2.0),
+                                         (40, 193, 16, 1.0), (3, 577, 4, 3.0), (7, 257, 5, 1.0)])
+def test_attention_persistent(B, L, H, scale):
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
+    qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    out = run_var(893, qkv, B, L, H)
+    ref = attn_ref(qkv, B, L, H, False)
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    assert (out - ref).abs().max().item() < tol
+    base = run_var(381, qkv, B, L, H)
+    assert (out - base).abs().max().item() < tol
+    assert torch.equal(out, run_var(893, qkv, B, L, H))
+
+
+def test_attention_persistent_spike():
+    """Dominant late keys in a few heads of a many-block grid: those waves leave the fixed offset
+    (general online softmax with rescales) while the others stay on it, across block seams."""
+    B, L, H = 24, 577, 16
+    g = torch.Generator(device="cpu").manual_seed(11)
+    qkv = torch.randn(B * L, 3 * H * 64, generator=g) * 0.5
+    D = H * 64
+    for b, h, q, k in ((0, 0, 10, 500), (5, 3, 300, 40), (23, 15, 576, 576), (11, 7, 0, 1)):
+        qkv[b * L + q, h * 64:(h + 1) * 64] = 4.0
+        qkv[b * L + k, D + h * 64:D + (h + 1) * 64] = 4.0
+    qkv = qkv.to(torch.bfloat16).to(DEV)
+    out = run_var(893, qkv, B, L, H)
+    ref = attn_ref(qkv, B, L, H, False)
+    assert (out - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())

@@ -60,7 +60,7 @@ def main():
         "out_v_f32": (Mv, 1024, 1024, 0, False, False), "proj_v_f32": (Mv, 1024, 4096, 0, False, False),
     }
     if args.only:
-        keep = set(args.only.split(","))
+        keep = set(args.only.replace("+", ",").split(","))
         shapes = {k: v for k, v in shapes.items() if k in keep}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     # bring the clocks up before the first timed shape (~2 s of dense bf16 matmul)
@@ -107,14 +107,18 @@ def main():
                 ms = timeit(lambda: torch.matmul(A, W.t(), out=Ob), args.reps)
                 res.setdefault(f"{name}/torch", []).append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
             del Ob
-    attns = {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B)}
+    attns = {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B),
+             # diagnostics: the same FLOPs at longer sequences (fewer, longer key loops per q-block)
+             "attn_v1153": (1153, 16, 0, B // 4), "attn_v2305": (2305, 16, 0, B // 16)}
     if args.only:
         attns = {k: v for k, v in attns.items() if k in keep}
+    else:
+        attns = {k: v for k, v in attns.items() if k in ("attn_v", "attn_t")}
     for attn, (L, H, causal, Bx) in attns.items():
         qkv = (torch.randn(Bx * L, 3 * H * 64, device="cuda", generator=g)).to(torch.bfloat16)
         out = torch.empty(Bx * L, H * 64, device="cuda", dtype=torch.bfloat16)
         for rnd in range(args.rounds):
-            for var in [int(v) for v in args.attn_vars.split(",")]:
+            for var in [int(v) for v in args.attn_vars.replace("+", ",").split(",")]:
                 _lib.lib().ce_set_attn_variant(var)
                 ms = timeit(lambda: _lib.call("ce_kernel_attention", stream, P(qkv), P(out), Bx, L, H, causal),
                             args.reps)

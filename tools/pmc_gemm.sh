@@ -7,7 +7,7 @@ ONLY=${1:-qkv_v,fc_v,out_v,proj_v,attn_v}
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" -d ${PMCDIR:-gpurun_out/pmc}/$name -o run --output-format csv -- \
-    python3 tools/bench_kernels.py --rounds 1 --reps 2 --warm-s 0 --scheds ${SCHEDS:-1} --only "$ONLY" > ${PMCDIR:-gpurun_out/pmc}/$name.log 2>&1
+    python3 tools/bench_kernels.py --rounds 1 --reps 2 --warm-s 0 --scheds ${SCHEDS:-1} --attn-vars ${ATTN_VARS:-381} --only "$ONLY" > ${PMCDIR:-gpurun_out/pmc}/$name.log 2>&1
 }
 mkdir -p ${PMCDIR:-gpurun_out/pmc}
 timeout -k 10 60 rocprofv3 -L > ${PMCDIR:-gpurun_out/pmc}/counters.txt 2>&1 || true
