@@ -967,6 +967,11 @@ int tgemm(ce_handle* h, hipStream_t s, const char* tag, const bf16_t* A, long ld
     return timed(h, s, tag, 2.0 * M * N * K, 0.0, [&] { return ce::launch_gemm(p, act, out_bf16, s); });
 }
 
+// activation backward in the dX_proj GEMM's epilogue (1, default) or as its own kernel (0)
+std::atomic<int> g_act_bwd_fuse{ce::kKnobUnset};     // A/B knob (knobs.h)
+int act_bwd_fuse_env() { return ce::env_int("CE_TRAIN_ACT_BWD_FUSE", 1) != 0; }
+bool act_bwd_fuse() { return ce::knob_get(g_act_bwd_fuse, act_bwd_fuse_env) != 0; }
+
 // weight gradients by the MN-major GEMM (gemm_tn.hip) or, 0, by transposed copies + the forward GEMM
 std::atomic<int> g_dw_tn{ce::kKnobUnset};     // A/B knob (knobs.h)
 int dw_tn_env() { return ce::env_int("CE_TRAIN_DW_TN", 1) != 0; }
@@ -1072,10 +1077,25 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
                          w.part));
         }
         CE_TRY(timed(h, s, "t_transpose", 0.0, 0.0, [&] { return ce::launch_transpose_bf16(w.WT, D, k.wproj, false, F, D, F, D, s); }));
-        CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
-        CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] {
-            return ce::launch_act_bwd_colsum(w.dA, w.pre[l], w.dA, M, F, act, G("mlp.c_fc.bias"), w.colsum, s);
-        }));
+        // dA = act'(pre) * (dres_b W_proj) and the c_fc bias gradient: one GEMM with the activation
+        // backward and the bias column sums in its epilogue where the default four-wave kernel takes
+        // this shape, else the GEMM then the activation-backward kernel (same values)
+        ce::GemmParams pb{};
+        pb.A = w.dres_b; pb.lda = D; pb.W = w.WT; pb.ldw = D;
+        pb.M = M; pb.N = F; pb.K = D;
+        pb.out = w.dA; pb.ldo = F;
+        pb.bwd_pre = w.pre[l]; pb.bwd_part = w.colsum;
+        if (act_bwd_fuse() && ce::gemm_act_bwd_fused(pb, act)) {
+            CE_TRY(timed(h, s, "dX_proj_act", 2.0 * M * F * D, 0.0, [&] { return ce::launch_gemm_act_bwd(pb, act, s); }));
+            CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] {
+                return ce::launch_colsum_finish(G("mlp.c_fc.bias"), w.colsum, (M + 127) / 128, F, s);
+            }));
+        } else {
+            CE_TRY(tgemm(h, s, "dX_proj", w.dres_b, D, w.WT, D, M, F, D, nullptr, 0, nullptr, w.dA, true, w.part));
+            CE_TRY(timed(h, s, "t_act_bwd", 0.0, 0.0, [&] {
+                return ce::launch_act_bwd_colsum(w.dA, w.pre[l], w.dA, M, F, act, G("mlp.c_fc.bias"), w.colsum, s);
+            }));
+        }
         if (tn) {
             CE_TRY(tgemm_tn(h, s, "dW_fc", w.dA, F, w.xn2[l], D, F, D, M, G("mlp.c_fc.weight"), w.part));
         } else {
@@ -2177,6 +2197,11 @@ int ce_set_attn_bwd_variant(int v) { return ce::set_attn_bwd_variant(v); }
 int ce_set_train_dw_tn(int on) {
     const int prev = dw_tn() ? 1 : 0;
     g_dw_tn.store(on ? 1 : 0);
+    return prev;
+}
+int ce_set_train_act_bwd_fuse(int on) {
+    const int prev = act_bwd_fuse() ? 1 : 0;
+    g_act_bwd_fuse.store(on ? 1 : 0);
     return prev;
 }
 int ce_kernel_gemm_tn_bf16(void* stream, const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K,

@@ -136,7 +136,34 @@ __device__ __forceinline__ float gelu_fast(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * p));
 }
 
-enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2 };
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_QGELU = 2,
+       // (device-side template codes of the activation-backward GEMM epilogue, launch_gemm_act_bwd:
+       // out = dh * act'(pre) for the GELU / QuickGELU forward activation)
+       ACT_GELU_BWD = 3, ACT_QGELU_BWD = 4 };
+
+// d/dx [x * Phi(x)] = Phi(x) + x phi(x), with erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
+// as erf_fast) sharing its one exponential with phi: exp(-a^2) = exp(-x^2 / 2) for a = |x| / sqrt(2).
+// One exp + one rcp + ~10 FMA per value instead of libm erff + expf: the activation backward over the
+// C4 batch's 363 M values was VALU-bound, not HBM-bound.
+// (v_rcp_f32, 1 ulp, in place of the IEEE-rounded reciprocal's 10-instruction division sequence:
+// t is in (0, 1], far inside the approximation's own 1.5e-7)
+__device__ __forceinline__ float gelu_grad(float x) {
+    const float a = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    p *= t;
+    const float e = __expf(-a * a);
+    const float erf_a = fmaf(-p, e, 1.0f);                               // erf(|x| / sqrt 2)
+    return fmaf(0.5f, copysignf(erf_a, x), 0.5f) + x * 0.3989422804014327f * e;
+}
+__device__ __forceinline__ float qgelu_grad(float x) {
+    const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+    return sg * (1.0f + 1.702f * x * (1.0f - sg));
+}
+
 
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {

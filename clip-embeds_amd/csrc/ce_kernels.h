@@ -59,6 +59,11 @@ struct GemmParams {
     // bf16 output with an activation (EPI_PLAIN, no residual): also store the pre-activation values
     // (bias added) here, same layout as out (the training forward keeps both for the backward)
     bf16_t* pre_out = nullptr;
+    // activation-backward epilogue (launch_gemm_act_bwd only): out = bf16(bf16(acc) * act'(bwd_pre))
+    // with bwd_pre the forward's pre-activation copy (same layout as out), and per 128-row block of
+    // the output the column sums of out into bwd_part[m / 128][n]
+    const bf16_t* bwd_pre = nullptr;
+    float* bwd_part = nullptr;
     // the process-wide schedule knobs (knobs.h), read once by launch_gemm so one launch never mixes
     // values another thread sets meanwhile
     struct {
@@ -69,6 +74,14 @@ struct GemmParams {
 // EPI_HL_F32: residual from hi/lo planes, plain f32 output (the tower's last residual GEMM)
 enum GemmEpi { EPI_PLAIN = 0, EPI_LN_STATS = 1, EPI_LN_FOLD = 2, EPI_LN_STATS_HL = 3, EPI_HL_F32 = 4 };
 hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t s, int epi = EPI_PLAIN);
+// dX GEMM of the MLP's c_proj in the text-tower backward with the activation backward and the c_fc
+// bias column sums in its epilogue (GemmParams::bwd_pre / bwd_part; act = the forward activation,
+// ACT_GELU or ACT_QGELU): the four-wave persistent kernel on the default policy, bf16 out, no bias /
+// residual, N % 128 == 0, out and bwd_pre of row stride N.  gemm_act_bwd_fused says whether a launch
+// would take it; launch_gemm_act_bwd returns hipErrorNotSupported otherwise (the caller then runs
+// launch_gemm + launch_act_bwd_colsum).  bwd_part holds (M + 127) / 128 rows of N floats.
+bool gemm_act_bwd_fused(const GemmParams& p, int act);
+hipError_t launch_gemm_act_bwd(const GemmParams& p, int act, hipStream_t s);
 // SCHED 13 (gemm_db.hip): bf16 output without residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0,
 // K >= 1024; `grid` persistent workgroups (p.gm set by the caller)
 hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipStream_t s);
@@ -254,7 +267,9 @@ hipError_t launch_ln_bwd(float* dres, const float* x, const float* dy, long ldy,
                          hipStream_t s, bf16_t* dres_b = nullptr, float* dsum = nullptr,
                          const bf16_t* dy_b = nullptr);   // dy_b: bf16 dy (row stride ldy) in place of dy
 // out = dh * act'(pre) over [M][N] bf16 and dbias = column sums of out (scratch >= act_bwd_colsum_scratch_floats)
-long act_bwd_colsum_scratch_floats(int M, int N);
+long act_bwd_colsum_scratch_floats(int M, int N);     // (also >= the fused GEMM's (M + 127) / 128 x N)
+// out[n] = sum over the nb rows of part[nb][N] (fixed order): the fused GEMM's bias-gradient partials
+hipError_t launch_colsum_finish(float* out, const float* part, int nb, int N, hipStream_t s);
 hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* dh, int M, int N, int act, float* dbias,
                                  float* scratch, hipStream_t s);
 // dh == nullptr: out = act(pre); else out = dh * act'(pre).  bf16, n % 8 == 0.

@@ -498,12 +498,103 @@ __device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f3
     }
 }
 
+// Activation-backward epilogue (ACT_GELU_BWD / ACT_QGELU_BWD, launch_gemm_act_bwd): the dX GEMM of
+// the MLP's c_proj in the text-tower backward (transformer.py:235-239 under autograd).  out =
+// bf16(bf16(acc) * act'(pre)) with pre the forward's pre-activation copy, and the column sums of
+// those bf16 outputs over the wave's 128 rows into bwd_part[mbase / 128][n]: the values, roundings
+// and bias-gradient inputs of launch_gemm + launch_act_bwd_colsum (train.hip), without writing and
+// re-reading the [M][F] product.  pre is read 16 B per lane at the output's own addresses (the
+// store layout below) and put back in fragment order by the inverse v_permlane16_swap; one 128-row
+// block of reads is in flight ahead of the one being consumed.  Column sums: each lane adds its 8
+// rows, then a reduce-scatter over the 16 lanes of a row group (DPP row_mirror, row_half_mirror,
+// quad_perm ^2, ^1) leaves lane fr with the finished sums of its 2 columns.  Whole 128-column quadrants.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// one reduce-scatter step over N value pairs: lanes with `hi` keep c[N..2N) (moved to c[0..N)), the
+// others c[0..N); each adds its partner's copy of the kept half
+template <int N, int CTRL>
+__device__ __forceinline__ void rs_step(float (&c)[32], bool hi) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const float send = hi ? c[k] : c[k + N];
+        const float keep = hi ? c[k + N] : c[k];
+        c[k] = keep + dpp_mov_f<CTRL>(send);
+    }
+}
+template <int ACT>
+__device__ __forceinline__ void w4_epilogue_act_bwd(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase,
+                                                    int nbase, int lane) {
+    if (mbase >= p.M) return;                                   // wave-uniform
+    const int fr = lane & 15, fq = lane >> 4;
+    const int rows = min(p.M - mbase, 128);
+    const __amdgpu_buffer_rsrc_t osrd =
+        make_srd(static_cast<bf16_t*>(p.out) + (size_t)mbase * p.ldo, rows * (int)p.ldo * 2);
+    const __amdgpu_buffer_rsrc_t psrd = make_srd(p.bwd_pre + (size_t)mbase * p.ldo, rows * (int)p.ldo * 2);
+    const int ldo2 = (int)p.ldo * 2;
+    const int voff0 = (fr + (fq & 1) * 16) * ldo2 + (fq >> 1) * 16 + nbase * 2;
+    float cs[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) cs[k] = 0.f;
+    u32x4 pv[2][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[0][j] = __builtin_amdgcn_raw_buffer_load_b128(psrd, voff0 + j * 32, 0, 0);
+    auto grad = [](float x) { return ACT == ACT_QGELU_BWD ? qgelu_grad(x) : gelu_grad(x); };
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) {
+        if (ip + 1 < 4) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                pv[(ip + 1) & 1][j] = __builtin_amdgcn_raw_buffer_load_b128(psrd, voff0 + (ip + 1) * 32 * ldo2 + j * 32, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32x4 d = pv[ip & 1][j];
+            // (h0, h1) of the store below, inverted: pre of rows 16r + fr, columns 16j + 4fq + 0..3
+            const auto px = __builtin_amdgcn_permlane16_swap(d[0], d[2], false, false);
+            const auto py = __builtin_amdgcn_permlane16_swap(d[1], d[3], false, false);
+            uint2 h[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const f32x4 v = acc[2 * ip + r][j];
+                const uint32_t d01 = pack_bf2(v[0], v[1]), d23 = pack_bf2(v[2], v[3]);   // dh as a bf16 GEMM output
+                const uint32_t p01 = px[r], p23 = py[r];
+                const float o0 = __uint_as_float(d01 << 16) * grad(__uint_as_float(p01 << 16));
+                const float o1 = __uint_as_float(d01 & 0xffff0000u) * grad(__uint_as_float(p01 & 0xffff0000u));
+                const float o2 = __uint_as_float(d23 << 16) * grad(__uint_as_float(p23 << 16));
+                const float o3 = __uint_as_float(d23 & 0xffff0000u) * grad(__uint_as_float(p23 & 0xffff0000u));
+                h[r] = make_uint2(pack_bf2(o0, o1), pack_bf2(o2, o3));
+                cs[4 * j + 0] += __uint_as_float(h[r].x << 16);
+                cs[4 * j + 1] += __uint_as_float(h[r].x & 0xffff0000u);
+                cs[4 * j + 2] += __uint_as_float(h[r].y << 16);
+                cs[4 * j + 3] += __uint_as_float(h[r].y & 0xffff0000u);
+            }
+            const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
+            const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
+            const u32x4 o = {x[0], y[0], x[1], y[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, osrd, voff0 + ip * 32 * ldo2 + j * 32, 0, 0);
+        }
+    }
+    // column c = 16j + 4fq + e of value k = 4j + e; after the four steps lane fr holds k = 2fr, 2fr + 1
+    rs_step<16, 0x140>(cs, (fr & 8) != 0);     // row_mirror: fr <-> 15 - fr
+    rs_step<8, 0x141>(cs, (fr & 4) != 0);      // row_half_mirror: fr <-> 7 - fr (within each 8)
+    rs_step<4, 0x4E>(cs, (fr & 2) != 0);       // quad_perm [2,3,0,1]
+    rs_step<2, 0xB1>(cs, (fr & 1) != 0);       // quad_perm [1,0,3,2]
+    const int col = nbase + 16 * (fr >> 1) + 4 * fq + 2 * (fr & 1);
+    *reinterpret_cast<float2*>(p.bwd_part + (size_t)(mbase >> 7) * p.N + col) = make_float2(cs[0], cs[1]);
+}
+
 template <int ACT, int EPI>
 __device__ __forceinline__ void w4_epilogue_bf16(const GemmParams& p, const f32x4 (&acc)[8][8], int mbase, int nbase,
                                                  int lane, const char* side) {
     if (nbase >= p.N) return;                                   // wave-uniform
-    if (p.N - nbase >= 128) w4_epilogue_bf16_n<ACT, EPI, 8>(p, acc, mbase, nbase, lane, side);
-    else w4_epilogue_bf16_n<ACT, EPI, 4>(p, acc, mbase, nbase, lane, side);   // N % 128 == 64
+    if constexpr (ACT == ACT_GELU_BWD || ACT == ACT_QGELU_BWD) {
+        w4_epilogue_act_bwd<ACT>(p, acc, mbase, nbase, lane);        // (launch_gemm_act_bwd: N % 128 == 0)
+    } else {
+        if (p.N - nbase >= 128) w4_epilogue_bf16_n<ACT, EPI, 8>(p, acc, mbase, nbase, lane, side);
+        else w4_epilogue_bf16_n<ACT, EPI, 4>(p, acc, mbase, nbase, lane, side);   // N % 128 == 64
+    }
 }
 
 // Four-wave epilogue of the residual GEMMs with LN statistics (out-proj / c_proj of the folded image
@@ -2759,6 +2850,30 @@ bool pre_out_fused(const GemmParams& p, int act) {
            !(p.variant & GEMM_VAR_W4_TAIL);
 }
 
+// knobs of one launch (launch_gemm's snapshot, GemmParams::kn)
+void snapshot_knobs(GemmParams& p) {
+    p.trace = g_trace;
+    p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
+    p.variant = gemm_variant();
+    p.kn.sched = gemm_sched();
+    p.kn.autom = gemm_auto();
+    p.kn.splitk = splitk_enabled() ? 1 : 0;
+    p.kn.groupm = gemm_groupm();
+    p.kn.stagger = gemm_stagger();
+    p.kn.ring = g_ring.load();
+    p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
+}
+
+// The activation-backward epilogue exists on the four-wave persistent kernel with the default
+// variant bits' DMA split (EV 3) only, without a split-K tail, for whole 128-column quadrants.
+bool act_bwd_fused_k(const GemmParams& p, int act) {
+    const int spread_alt = GEMM_VAR_W4_SPREAD12 | GEMM_VAR_W4_SPREAD8 | GEMM_VAR_W4_SPREAD_EVEN;
+    return (act == ACT_GELU || act == ACT_QGELU) && p.bwd_pre && p.bwd_part && p.out && !p.bias && !p.resid &&
+           !p.rhl && !p.pre_out && !p.m_dev && !p.grp && !p.onetile && p.M > 0 && p.ldo == p.N && p.N % 128 == 0 &&
+           p.K > 0 && p.K % BK == 0 && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
+           (p.variant & GEMM_VAR_W4_DMA_SPREAD) && !(p.variant & spread_alt) && !(p.variant & GEMM_VAR_W4_TAIL);
+}
+
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
@@ -2901,18 +3016,34 @@ void set_gemm_trace(unsigned long long* buf, long n) {
     g_trace_n = buf ? n : 0;
 }
 
+bool gemm_act_bwd_fused(const GemmParams& p0, int act) {
+    GemmParams p = p0;
+    snapshot_knobs(p);
+    return act_bwd_fused_k(p, act);
+}
+
+hipError_t launch_gemm_act_bwd(const GemmParams& p0, int act, hipStream_t s) {
+    GemmParams p = p0;
+    snapshot_knobs(p);
+    if (!act_bwd_fused_k(p, act)) return hipErrorNotSupported;
+    p.gm = p.kn.groupm;
+    p.stagger = p.kn.stagger;
+    const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
+    const int grid = w4pp_grid(p, nwg);
+    plan_tail_w4(p, nwg, grid);
+    if (p.tail) return hipErrorNotSupported;      // (W4_TAIL is off: unreachable)
+    if (act == ACT_GELU)
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_GELU_BWD, false, true, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_QGELU_BWD, false, true, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
+    count_path(GEMM_PATH_W4PP + EPI_PLAIN);
+    return hipGetLastError();
+}
+
 hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t s, int epi) {
     GemmParams p = p0;
-    p.trace = g_trace;
-    p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
-    p.variant = gemm_variant();
-    p.kn.sched = gemm_sched();
-    p.kn.autom = gemm_auto();
-    p.kn.splitk = splitk_enabled() ? 1 : 0;
-    p.kn.groupm = gemm_groupm();
-    p.kn.stagger = gemm_stagger();
-    p.kn.ring = g_ring.load();
-    p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
+    snapshot_knobs(p);
+    if (p.bwd_pre || p.bwd_part) return hipErrorInvalidValue;   // launch_gemm_act_bwd only
     if (p.M <= 0 || p.N <= 0) return hipSuccess;
     if (p.m_dev) {
         // packed rows: the folded-tower epilogues on one tile per workgroup, no split-K; only the default

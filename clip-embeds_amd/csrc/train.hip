@@ -233,26 +233,6 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dres, const 
 
 // ---------------------------------------------------------------------------------------------
 // Activation forward (h = act(pre)) and backward (dpre = dh * act'(pre)), bf16, 8 per thread.
-// d/dx [x * Phi(x)] = Phi(x) + x phi(x), with erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
-// as erf_fast) sharing its one exponential with phi: exp(-a^2) = exp(-x^2 / 2) for a = |x| / sqrt(2).
-// One exp + one rcp + ~10 FMA per value instead of libm erff + expf: the activation backward over the
-// C4 batch's 363 M values was VALU-bound, not HBM-bound.
-__device__ __forceinline__ float gelu_grad(float x) {
-    const float a = fabsf(x) * 0.70710678118654752f;
-    const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
-    float p = fmaf(1.061405429f, t, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    p *= t;
-    const float e = __expf(-a * a);
-    const float erf_a = fmaf(-p, e, 1.0f);                               // erf(|x| / sqrt 2)
-    return fmaf(0.5f, copysignf(erf_a, x), 0.5f) + x * 0.3989422804014327f * e;
-}
-__device__ __forceinline__ float qgelu_grad(float x) {
-    const float sg = 1.0f / (1.0f + __expf(-1.702f * x));
-    return sg * (1.0f + 1.702f * x * (1.0f - sg));
-}
 template <int ACT, bool BWD>
 __global__ __launch_bounds__(256) void act_k(bf16_t* __restrict__ out, const bf16_t* __restrict__ pre,
                                              const bf16_t* __restrict__ dh, long n8) {
@@ -1053,7 +1033,13 @@ int act_colsum_chunk(int M, int N) {
     return std::max(16, (M + target - 1) / target);
 }
 long act_bwd_colsum_scratch_floats(int M, int N) {
-    return (long)((M + act_colsum_chunk(M, N) - 1) / act_colsum_chunk(M, N)) * N;
+    const long unfused = (long)((M + act_colsum_chunk(M, N) - 1) / act_colsum_chunk(M, N)) * N;
+    return std::max(unfused, (long)((M + 127) / 128) * N);
+}
+hipError_t launch_colsum_finish(float* out, const float* part, int nb, int N, hipStream_t s) {
+    if (nb <= 0 || N <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(colsum_finish_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, out, part, nb, N, 1.0f, 0);
+    return hipGetLastError();
 }
 hipError_t launch_act_bwd_colsum(bf16_t* out, const bf16_t* pre, const bf16_t* dh, int M, int N, int act, float* dbias,
                                  float* scratch, hipStream_t s) {

@@ -341,6 +341,11 @@ int ce_kernel_gemm_tn_bf16(void* stream, const void* A, int64_t lda, const void*
 /* Text-tower training: weight gradients by the MN-major GEMM above (1, default) or by transposed
  * operand copies and the forward GEMM (0, the round-3 path).  Returns the previous setting.  For A/B. */
 int ce_set_train_dw_tn(int on);
+/* Text-tower training: the MLP's activation backward (dpre = dh * act'(pre)) and the c_fc bias
+ * gradient in the epilogue of the dX GEMM that produces dh (1, default, where the four-wave kernel
+ * takes that GEMM) or as a separate kernel over the GEMM's bf16 output (0).  Same dpre values; the
+ * bias sums differ in f32 summation order only.  Returns the previous setting.  For A/B. */
+int ce_set_train_act_bwd_fuse(int on);
 /* f32 GEMM kernel of the projections, logits and SPARC einsums (pacl.py:460,472): 1 = the
  * register-blocked 96 x 128 kernel (default; 16-B aligned operands with K % 4 == 0); 2 = as 1, and
  * for batched products of M <= 80 rows and N >= 192 (SPARC's T = 77 rows per sample) the 80 x 192

@@ -77,8 +77,14 @@ def c4():
         L.ce_set_gemm_auto(pa)
         L.ce_set_gemm_splitk(ps)
         L.ce_set_train_dw_tn(pt)
+    pf = L.ce_set_train_act_bwd_fuse(0)
+    try:
+        loss_unfused, g_unfused = run()
+    finally:
+        L.ce_set_train_act_bwd_fuse(pf)
     return dict(m=m, tr=tr, img=img, caps=caps, loss_big=loss_big, g_big=g_big, cnt_big=cnt_big,
-                loss_plain=loss_plain, g_plain=g_plain, cnt_plain=cnt_plain)
+                loss_plain=loss_plain, g_plain=g_plain, cnt_plain=cnt_plain, loss_unfused=loss_unfused,
+                g_unfused=g_unfused)
 
 
 def _views(tr, flat):
@@ -140,3 +146,19 @@ def test_matches_f32_autograd_restatement(c4):
         if not (c >= 0.995 and abs(nr - 1) < 0.03):
             bad.append((n, round(c, 5), round(nr, 4)))
     assert not bad, bad
+
+
+def test_act_backward_fused_matches_separate_kernel(c4):
+    """The activation backward in the dX_proj GEMM's epilogue (launch_gemm_act_bwd) vs the GEMM then
+    launch_act_bwd_colsum: the same bf16 dpre values, so every gradient but the c_fc biases is
+    bitwise identical; the c_fc bias sums (per 128-row block + DPP reduce-scatter vs per row chunk)
+    differ in f32 summation order only."""
+    assert c4["loss_big"] == c4["loss_unfused"]
+    vb, vu = _views(c4["tr"], c4["g_big"]), _views(c4["tr"], c4["g_unfused"])
+    for n in vb:
+        if n.endswith("mlp.c_fc.bias"):
+            d = (vb[n] - vu[n]).abs().max().item()
+            assert d <= 1e-5 * max(vu[n].abs().max().item(), 1e-12), (n, d)
+        else:
+            assert torch.equal(vb[n], vu[n]), n
+
