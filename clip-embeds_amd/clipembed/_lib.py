@@ -110,6 +110,7 @@ _SIGNATURES = {
     "ce_kernel_gemm_tn_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
                                        c_int64, c_int, c_float]),
     "ce_set_train_dw_tn": (c_int, [c_int]),
+    "ce_set_train_act_bwd_fuse": (c_int, [c_int]),
     "ce_set_gemm_trace": (c_int, [c_void_p, c_int64]),
     "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),
