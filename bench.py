@@ -135,17 +135,20 @@ def load_traffic(tag):
 
 def load_mfma_busy(tag):
     """Counter-based MFMA utilisation of `tag` (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE, one rocprofv3
-    --pmc pass over this bench; tools/summarize_mfma.py -> profiles/r04/mfma_busy.json), if measured."""
-    path = os.path.join(REPO, "profiles", "r04", "mfma_busy.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)["kernels"].get(tag)
-    except (OSError, ValueError, KeyError):
-        return None
-    if not d:
-        return None
-    return {"mfma_busy": d["mfma_busy"], "clock_GHz": d["clock_GHz"], "frac_at_nominal": d["frac_at_nominal"],
-            "source": "profiles/r04/mfma_busy.json"}
+    --pmc pass over this bench; tools/summarize_mfma.py -> profiles/<round>/mfma_busy.json, the latest
+    round that has one), if measured."""
+    for rnd in ("r05", "r04"):
+        path = os.path.join(REPO, "profiles", rnd, "mfma_busy.json")
+        try:
+            with open(path) as f:
+                d = json.load(f)["kernels"].get(tag)
+        except (OSError, ValueError, KeyError):
+            continue
+        if not d:
+            continue
+        return {"mfma_busy": d["mfma_busy"], "clock_GHz": d["clock_GHz"], "frac_at_nominal": d["frac_at_nominal"],
+                "source": f"profiles/{rnd}/mfma_busy.json"}
+    return None
 
 
 # ----------------------------------------------------------------------------------- workloads
