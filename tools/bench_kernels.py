@@ -109,7 +109,9 @@ def main():
             del Ob
     attns = {"attn_v": (577, 16, 0, B), "attn_t": (77, 12, 1, B),
              # diagnostics: the same FLOPs at longer sequences (fewer, longer key loops per q-block)
-             "attn_v1153": (1153, 16, 0, B // 4), "attn_v2305": (2305, 16, 0, B // 16)}
+             "attn_v1153": (1153, 16, 0, B // 4), "attn_v2305": (2305, 16, 0, B // 16),
+             # the image shape at smaller batches (K / V of every head within the 256-MB MALL)
+             "attn_v_b64": (577, 16, 0, B // 4), "attn_v_b32": (577, 16, 0, B // 8)}
     if args.only:
         attns = {k: v for k, v in attns.items() if k in keep}
     else:
