@@ -78,7 +78,9 @@ template <bool CAUSAL, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int Lp, int H,
                                                     float qscale, float* __restrict__ lse,
-                                                    const int* __restrict__ seg) {
+                                                    const int* __restrict__ seg,
+                                                    unsigned long long* __restrict__ trace = nullptr,
+                                                    int trace_n = 0) {
     constexpr bool RING3 = (VAR & 128) != 0;  // three K/V slots: tile t+2 in flight beside t+1 (ONEBAR)
     __shared__ __attribute__((aligned(16))) char smem[(RING3 ? 3 : 2) * STAGE_BYTES];
     constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
@@ -92,6 +94,36 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     // key tiles cover keys 1..L-1: L = 577 runs 9 full tiles instead of 9 + one single-key tile on the
     // masked general path
     constexpr bool CLSK = !CAUSAL && (VAR & 256) != 0;
+    constexpr bool EARLY = (VAR & 2048) != 0;
+    // TRACE (bit 1024, diagnostics, ce_set_attn_trace): lane 0 of every wave records s_memrealtime
+    // (100 MHz) at entry, after the prologue (Q, key 0), after tile 0's wait, after the tile loop and
+    // after the stores, plus (XCC id << 32 | HW_ID), into its own 8-word record (vector stores)
+    constexpr bool TRACE = (VAR & 1024) != 0;
+    unsigned long long* trec = nullptr;
+    if constexpr (TRACE) {
+        const long rec = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (trace && rec < trace_n) trec = trace + rec * 8;
+    }
+    auto stamp = [&](int slot) {
+        if constexpr (TRACE) {
+            if (trec && (threadIdx.x & 63) == 0) {
+                unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                asm volatile("" : "+v"(t));
+                trec[slot] = t;
+            }
+        }
+    };
+    stamp(0);
+    if constexpr (TRACE) {
+        if (trec && (threadIdx.x & 63) == 0) {
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            unsigned long long id = ((unsigned long long)xcc << 32) | hw;
+            asm volatile("" : "+v"(id));
+            trec[5] = id;
+        }
+    }
 
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
@@ -123,22 +155,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int h2 = lane >> 5;
     const int qrow = qb * QBLK + wave * 32 + r;
     const int q_wave0 = qb * QBLK + wave * 32;        // first query of this wave (wave-uniform)
-
-    // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
-    bf16x8 qf[4];
-    {
-        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-        // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
-        // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
-        if (qscale != 1.0f) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
-        }
-    }
 
     // staging: thread -> row tid>>3 of a 32-row pass, 16-B chunk tid&7
     const int srow = tid >> 3;
@@ -186,6 +202,46 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             glds16(vbase + (size_t)key * ld + vchunk * 8, dst + TILE_KV_BYTES + ps * 4096);
         }
     };
+
+    // EARLY (bit 2048): tile 0's K / V DMA goes out before the Q and key-0 loads, and those loads are
+    // all issued before the first use of any of them, so the wave waits for one memory latency at
+    // entry instead of three in a row (Q, then key 0, then tile 0: tools/attn_trace.py measured
+    // 4.6 us of prologue + 2.7 us of tile-0 wait per 32-query wave against 15 us of key tiles at
+    // L = 577)
+    if constexpr (EARLY) {
+        stage(0, 0);
+        if constexpr (RING3) {
+            if (nkt > 1) stage(1, 1);
+        }
+    }
+    // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
+    bf16x8 qf[4];
+    {
+        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+    }
+    // key 0's K row (CLSK) and V row words, loaded with Q (EARLY) so their latencies overlap
+    bf16x8 k0v[4];
+    uint2 v0w[2][4];
+    if constexpr (CLSK && EARLY) {
+        const bf16_t* k0 = base + D + h * 64 + 8 * h2;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) k0v[ks] = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+        const bf16_t* v0 = base + 2 * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) v0w[dt][g] = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
+    }
+    // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
+    // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
+    if (qscale != 1.0f) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
+    }
 
     // per-lane LDS read offsets
     int koff[2][4];
@@ -235,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         float a = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-            const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+            const bf16x8 kv = EARLY ? k0v[ks] : *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
             // v_dot2_f32_bf16 on the bf16 pairs: 16 instructions instead of 32 FMAs + 64 unpacks
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -255,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
+                const uint2 w = EARLY ? v0w[dt][g] : *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
                 const f32x2 pp = {p0, p0};
                 const f32x2 x0 = f32x2{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u)} * pp;
                 const f32x2 x1 = f32x2{__uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)} * pp;
@@ -338,9 +394,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         m_run += delta;
     };
 
-    stage(0, 0);
-    if constexpr (RING3) {
-        if (nkt > 1) stage(1, 1);
+    stamp(1);
+    if constexpr (!EARLY) {
+        stage(0, 0);
+        if constexpr (RING3) {
+            if (nkt > 1) stage(1, 1);
+        }
     }
     // one key tile; BUF (the ring slot, t & 1, or t % 3 with RING3) is a compile-time constant so
     // every LDS address is a per-lane offset plus an immediate (the loop is unrolled by two / three)
@@ -358,6 +417,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             // slot BUF^1 then takes tile t+1
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             barrier();
+            if (t == 0) stamp(2);
             if (t + 1 < nkt) stage(t + 1, BUF ^ 1);
         } else {
             if (t + 1 < nkt) {
@@ -536,6 +596,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         }
     }
 
+    stamp(3);
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (MODE == 2 ? lm[0] : 0.f);
     const float inv = 1.0f / l_tot;
@@ -576,6 +637,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 *reinterpret_cast<uint2*>(op + d0) = w;
             }
     }
+    if constexpr (TRACE) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(4);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -591,10 +656,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 // c ^ (r & 7): conflict-free ds_read_b128 of 8 rows), key 0's K and V rows (one DMA, 1 KB written).
 template <int VAR>
 __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                     int L, int H, int nblk, float qscale) {
+                                                     int L, int H, int nblk, float qscale,
+                                                     unsigned long long* __restrict__ trace = nullptr,
+                                                     int trace_n = 0, int* __restrict__ sched = nullptr) {
+    // DYN (bit 4096): blocks handed out at run time from per-XCD counters (sched[0..7]; sched[8]
+    // counts finished workgroups, and the last one resets all nine to 0 for the next launch) instead
+    // of the static rounds: a static assignment runs as long as its slowest CU, and per-wave block
+    // times spread by +-15 % (tools/attn_trace.py --var 1917: the waves' mean 403 us against a 513-us
+    // launch).  XCD x serves blocks [x nblk / 8, (x + 1) nblk / 8) first (the q-blocks of a head stay
+    // on one L2), then the other XCDs' ranges.  A workgroup learns its next block at the start of
+    // the current one (wave 0, published through LDS at tile 1's barrier)
+    constexpr bool DYN = (VAR & 4096) != 0;
+    // TRACE (bit 1024, diagnostics): per wave, the s_memrealtime time spent in block starts (the
+    // counted wait + barrier + Q / key-0 reads), in key-tile loops and in epilogues, and the block
+    // count, summed over the wave's blocks: trace[(block * 4 + wave) * 4 + 0..3]
+    constexpr bool TRACE = (VAR & 1024) != 0;
+    unsigned long long tr_wait = 0, tr_loop = 0, tr_epi = 0, tr_n = 0, tr_t = 0;
+    auto now = [&]() -> unsigned long long {
+        unsigned long long t = 0;
+        if constexpr (TRACE) {
+            t = __builtin_amdgcn_s_memrealtime();
+            asm volatile("" : "+s"(t));
+        }
+        return t;
+    };
     constexpr int QOFF = 2 * STAGE_BYTES;
     constexpr int COFF = QOFF + QBLK * 128;
-    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024];
+    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024 + 16];
+    int* const s_next = reinterpret_cast<int*>(smem + COFF + 1024);
     // blocks slot, slot + G, slot + 2G, ...: the grid walks the blocks in rounds, and slot is the XCD-aware
     // remap of attn_fwd, so the q-blocks of one (batch, head) run at the same time on one XCD and
     // share its K / V tiles in that XCD's L2 (contiguous runs per workgroup re-read every head's K / V
@@ -602,8 +691,53 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     const int G = gridDim.x;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qn = G >> 3, rn = G & 7;
-    const int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
-    if (blk_first >= nblk) return;        // workgroup-uniform
+    // wave 0, lane 0: the next block from the counters (-1: none left), written to s_next.  Split so
+    // the common case's atomic has a key tile to return: grab_issue (own XCD's counter) at a block's
+    // start, grab_finish at the end of its tile 0 (the other XCDs' counters, in turn, only once the own
+    // range is used up)
+    const int own_lo = (int)((long)xcd * nblk / 8), own_hi = (int)((long)(xcd + 1) * nblk / 8);
+    // The block-start atomic's result is consumed by every lane (lanes other than 0 hold the "no block"
+    // value): a use on lane 0's path only would leave the atomic pending, for the compiler's wait
+    // analysis, on the path that skips it, and hipcc then waits for it (and, in vmcnt's issue order,
+    // for the previous block's output stores) at the loop head.  (Inline asm instead lets hipcc copy
+    // the result register before the atomic has written it: blocks were lost.)
+    auto grab_issue = [&](int& dyn_k) __attribute__((always_inline)) {
+        if constexpr (DYN) {
+            dyn_k = 1 << 30;
+            if (threadIdx.x == 0 && own_lo < own_hi) dyn_k = atomicAdd(&sched[xcd], 1);
+        }
+    };
+    auto grab_finish = [&](int dyn_k) __attribute__((always_inline)) {
+        if constexpr (DYN) {
+            int got = dyn_k < own_hi - own_lo ? own_lo + dyn_k : -1;
+            if (threadIdx.x == 0) {
+                for (int j = 1; j < 8 && got < 0; ++j) {
+                    const int x = (xcd + j) & 7;
+                    const int lo = (int)((long)x * nblk / 8), hi = (int)((long)(x + 1) * nblk / 8);
+                    if (lo >= hi) continue;
+                    const int kk = atomicAdd(&sched[x], 1);
+                    if (lo + kk < hi) got = lo + kk;
+                }
+                *s_next = got;
+            }
+        }
+    };
+    int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    if constexpr (DYN) {
+        int k0 = 0;
+        grab_issue(k0);
+        grab_finish(k0);
+        barrier();
+        blk_first = *s_next;
+        barrier();                        // (every wave read it before wave 0's next grab overwrites it)
+        if (blk_first < 0) {
+            if (threadIdx.x == 0 && atomicAdd(&sched[8], 1) == G - 1)
+                for (int i = 0; i < 9; ++i) sched[i] = 0;
+            return;                       // workgroup-uniform
+        }
+    } else {
+        if (blk_first >= nblk) return;    // workgroup-uniform
+    }
     const int nqb = (L + QBLK - 1) / QBLK;
     const int D = H * 64;
     const int ld2 = 6 * D;                // bytes per qkv row
@@ -658,7 +792,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
         int ocol;
         const char* hb;
     };
-    auto decode = [&](int bk) {
+    auto decode = [&](int bk) __attribute__((always_inline)) {
         Blk k;
         const int bh = bk / nqb;
         k.qb = bk - bh * nqb;
@@ -668,7 +802,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
         k.hb = reinterpret_cast<const char*>(qkv) + (size_t)b * L * ld2 + h * 128;
         return k;
     };
-    auto stage_kv = [&](int t, auto bufc, __amdgpu_buffer_rsrc_t ks_, __amdgpu_buffer_rsrc_t vs_) {
+    auto stage_kv = [&](int t, auto bufc, __amdgpu_buffer_rsrc_t ks_, __amdgpu_buffer_rsrc_t vs_) __attribute__((always_inline)) {
         constexpr int BUF = decltype(bufc)::value;
         char* dst = smem + BUF * STAGE_BYTES + wave * 1024;
         const int ro = t * KBLK * ld2;
@@ -682,7 +816,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     };
     // Q rows (clamped to L - 1: the lanes past the end compute row L - 1's values again) and key 0's
     // K / V rows (wave 0: lanes 0-7 K, 8-15 V, the rest repeat them into the area's unused bytes)
-    auto stage_q = [&](int qb, __amdgpu_buffer_rsrc_t qs_) {
+    auto stage_q = [&](int qb, __amdgpu_buffer_rsrc_t qs_) __attribute__((always_inline)) {
 #pragma unroll
         for (int ps = 0; ps < 4; ++ps) {
             const int row = min(qb * QBLK + wave * 32 + ps * 8 + (lane >> 3), L - 1);
@@ -706,16 +840,32 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     bool stores_out = false;              // the previous block's 4 output stores may be in flight
     const f32x16 zero16 = {};
 
-    for (int blk = blk_first; blk < nblk; blk += G) {
+    if constexpr (TRACE) tr_t = now();
+    for (int blk = blk_first; blk >= 0 && blk < nblk;) {
         // this block's Q, key-0 rows and K/V tile 0 landed (counted: the 4 stores after them may not)
         if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier();
-        const bool has_next = blk + G < nblk;
-        const Blk nxt = decode(has_next ? blk + G : blk);
-        const __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
-        const __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
-        const __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
+        // next block: static rounds, or (DYN) grabbed now (the atomic returns under tile 0; wave 0
+        // publishes it at the end of tile 0 and every wave reads it after tile 1's barrier)
+        int dyn_k = 0;
+        if constexpr (DYN) grab_issue(dyn_k);
+        int nblk_id = blk + G;
+        bool has_next = !DYN && nblk_id < nblk;
+        Blk nxt = decode(has_next ? nblk_id : blk);
+        __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
+        __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
+        __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
+        auto learn_next = [&]() __attribute__((always_inline)) {
+            if constexpr (DYN) {
+                nblk_id = __builtin_amdgcn_readfirstlane(*s_next);
+                has_next = nblk_id >= 0;
+                nxt = decode(has_next ? nblk_id : blk);
+                nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
+                nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
+                nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
+            }
+        };
         const int q_wave0 = cur.qb * QBLK + wave * 32;
         const int qrow = q_wave0 + r;
         const bool active = q_wave0 < L;  // wave-uniform
@@ -786,7 +936,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     CE_TRV((Q) & 1, 0, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024); \
     CE_TRV((Q) & 1, 1, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
     CE_TRV((Q) & 1, 1, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024)
-            auto mf = [&](int q) {
+            auto mf = [&](int q) __attribute__((always_inline)) {
 #pragma unroll
                 for (int dt = 0; dt < 2; ++dt) {
                     const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -807,27 +957,38 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
 #undef CE_ISSUE
 #undef CE_TRV
         };
-        auto rescale = [&](float delta) {
+        auto rescale = [&](float delta) __attribute__((always_inline)) {
             const float alpha = __builtin_amdgcn_exp2f(-delta);
             l_run *= alpha;
 #pragma unroll
             for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
             m_run += delta;
         };
-        auto tile = [&](const int t, auto bufc) {
+        auto tile = [&](const int t, auto bufc) __attribute__((always_inline)) {
             constexpr int BUF = decltype(bufc)::value;
             // tile t landed and every wave is done with tile t - 1 (tile 0: the block-start barrier; with a
             // single tile, the Q / key-0 reads before the next block's DMAs overwrite them)
+            // the next block's Q / key-0 rows are staged at tile qt (tile 1 when there are >= 3 tiles:
+            // every wave has read this block's Q by tile 1's barrier), behind that tile's K / V DMAs, so
+            // tile qt + 1 waits for its own K / V only (counted: the Q pieces issued after them stay in
+            // flight) and they have two tiles to land; with fewer tiles, at the last tile
+            const int qt = nkt >= 3 ? 1 : nkt - 1;      // (DYN: nkt >= 3, launcher)
             if (t > 0 || nkt == 1) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (t == qt + 1 && has_next) {
+                    if (wave == 0) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                }
                 barrier();
             }
+            if (DYN && t == 1) learn_next();      // (wave 0 wrote s_next before this barrier: grab_finish)
             if (t + 1 < nkt) {
                 stage_kv(t + 1, std::integral_constant<int, BUF ^ 1>{}, ksrd, vsrd);
             } else if (has_next) {
                 stage_kv(0, std::integral_constant<int, BUF ^ 1>{}, nksrd, nvsrd);
-                stage_q(nxt.qb, nqsrd);
             }
+            if (t == qt && has_next) stage_q(nxt.qb, nqsrd);
             const char* kb = smem + BUF * STAGE_BYTES;
             bool redo = false;
             const bool fast_tile = fast;   // wave-uniform
@@ -908,16 +1069,31 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
                 l_run += psum;
                 pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
             }
+            if constexpr (DYN) {
+                if (t == 0) grab_finish(dyn_k);
+            }
         };
-        auto run = [&](auto pc) {
+        auto run = [&](auto pc) __attribute__((always_inline)) {
             constexpr int P = decltype(pc)::value;
             for (int t = 0; t < nkt; t += 2) {
                 tile(t, std::integral_constant<int, P>{});
                 if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, P ^ 1>{});
             }
         };
+        unsigned long long tl0 = 0;
+        if constexpr (TRACE) {
+            tl0 = now();
+            tr_wait += tl0 - tr_t;
+        }
         if (par) run(std::integral_constant<int, 1>{});
         else run(std::integral_constant<int, 0>{});
+        // (a use of the block-start atomic's result on every path, so the compiler's wait analysis
+        // never carries it pending round the loop: it would wait for it at the loop head)
+        if constexpr (DYN) asm volatile("" : : "v"(dyn_k));
+        if constexpr (TRACE) {
+            tr_t = now();
+            tr_loop += tr_t - tl0;
+        }
 
         // epilogue: O = O^T / l, 16-B stores (lanes l, l^32 trade halves); rows past L repeat row L - 1
         if (active) {
@@ -942,13 +1118,39 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
                 }
         }
         stores_out = active;
+        if constexpr (TRACE) {
+            const unsigned long long te = now();
+            tr_epi += te - tr_t;
+            tr_t = te;
+            ++tr_n;
+        }
         cur = nxt;
         qsrd = nqsrd; ksrd = nksrd; vsrd = nvsrd;
         par ^= nkt & 1;
+        blk = has_next ? nblk_id : -1;
+    }
+    if constexpr (DYN) {
+        // the last workgroup out resets the counters (every other one has finished its grabs)
+        if (threadIdx.x == 0 && atomicAdd(&sched[8], 1) == G - 1)
+            for (int i = 0; i < 9; ++i) sched[i] = 0;
+    }
+    if constexpr (TRACE) {
+        const long rec = (long)blockIdx.x * 4 + wave;
+        if (trace && rec < trace_n && lane == 0) {
+            unsigned long long v[4] = {tr_wait, tr_loop, tr_epi, tr_n};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                asm volatile("" : "+v"(v[k]));
+                trace[rec * 4 + k] = v[k];
+            }
+        }
     }
 }
 
 std::atomic<int> g_attn_var{381};     // A/B knob (knobs.h: process-wide atomic)
+// diagnostics (ce_set_attn_trace): per-wave timeline of variant 1405 (= 381 with TRACE) launches
+std::atomic<unsigned long long*> g_attn_trace{nullptr};
+std::atomic<long> g_attn_trace_n{0};
 
 // One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
 // mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
@@ -1090,7 +1292,7 @@ hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* ou
 }
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s, float* lse, const int* seg) {
+                            hipStream_t s, float* lse, const int* seg, int* sched) {
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
@@ -1098,7 +1300,8 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
     const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
-    if (!causal && v == 893 && clsk_ok && !lse && !seg) {
+    const bool dyn = v == 4989 && (L - 1) / KBLK >= 3;
+    if (!causal && (v == 893 || v == 1917 || dyn) && clsk_ok && !lse && !seg) {
         // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
         static std::atomic<int> occ[kMaxDevices];
         const int dev = current_device();
@@ -1117,7 +1320,28 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         const long nblk = (long)((L + QBLK - 1) / QBLK) * H * B;
         if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
         const int g = (int)std::min<long>(nblk, (long)per_cu * device_cus());
-        hipLaunchKernelGGL((attn_fwd_p<893>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
+        if (dyn) {
+            // the caller's 9 zeroed ints (left zeroed by the kernel), or a stream-ordered temporary
+            int* sc = sched;
+            if (!sc) {
+                hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&sc), 64, s);
+                if (e == hipSuccess) e = hipMemsetAsync(sc, 0, 64, s);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL((attn_fwd_p<4989>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
+                               nullptr, 0, sc);
+            const hipError_t e = hipGetLastError();
+            if (!sched) {
+                const hipError_t f = hipFreeAsync(sc, s);
+                if (e == hipSuccess && f != hipSuccess) return f;
+            }
+            return e;
+        }
+        if (v == 1917)
+            hipLaunchKernelGGL((attn_fwd_p<1917>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
+                               g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
+        else
+            hipLaunchKernelGGL((attn_fwd_p<893>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
         return hipGetLastError();
     }
     if (causal) {
@@ -1127,9 +1351,20 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = v == 893 ? (clsk_ok ? 381 : 125) : (v & 256) && !clsk_ok ? (v & ~256) : v;
+        const int vv = (v == 893 || v == 1917 || v == 4989) ? (clsk_ok ? 381 : 125)
+                     : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
+                     : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
             case 381: CE_ATTN_LAUNCH(false, 381); break;
+            case 2429: CE_ATTN_LAUNCH(false, 2429); break;
+            case 3453:
+                hipLaunchKernelGGL((attn_fwd<false, 3453>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg,
+                                   g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
+                break;
+            case 1405:
+                hipLaunchKernelGGL((attn_fwd<false, 1405>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg,
+                                   g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
+                break;
             case 125: CE_ATTN_LAUNCH(false, 125); break;
             case 253: CE_ATTN_LAUNCH(false, 253); break;
             case 61: CE_ATTN_LAUNCH(false, 61); break;
@@ -1151,10 +1386,16 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     return hipGetLastError();
 }
 
+void set_attn_trace(unsigned long long* buf, long n) {
+    g_attn_trace_n.store(buf ? n : 0);
+    g_attn_trace.store(buf);
+}
+
 int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61 || var == 125 || var == 253 || var == 381 || var == 893)
+                  var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
+                  var == 3453 || var == 1917 || var == 4989)
                      ? var : 381;
     return prev;
 }

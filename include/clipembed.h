@@ -376,6 +376,11 @@ int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, i
  * and every later GEMM launch of every handle and stream writes through it: diagnostics only, one
  * stream at a time, and call ce_set_gemm_trace(NULL, 0) (after a sync) before freeing buf. */
 int ce_set_gemm_trace(void* buf, int64_t n_blocks);
+/* Diagnostics: attention variant 1405 (= 381 with a timeline; ce_set_attn_variant) records per wave
+ * {s_memrealtime at entry, after the prologue (Q, key 0), after tile 0's wait, after the key-tile
+ * loop, after the output stores, (XCC id << 32) | HW_ID, -, -} into buf (device, n_waves x 8 uint64;
+ * record = block * 4 + wave) for records < n_waves.  Same process-wide contract as ce_set_gemm_trace. */
+int ce_set_attn_trace(void* buf, int64_t n_waves);
 /* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
  * stats [rows] float2, part [rows][nslab] float2. */
 int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab);
