@@ -668,8 +668,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     // the current one (wave 0, published through LDS at tile 1's barrier)
     constexpr bool DYN = (VAR & 4096) != 0;
     // TRACE (bit 1024, diagnostics): per wave, the s_memrealtime time spent in block starts (the
-    // counted wait + barrier + Q / key-0 reads), in key-tile loops and in epilogues, and the block
-    // count, summed over the wave's blocks: trace[(block * 4 + wave) * 4 + 0..3]
+    // counted wait + barrier + Q / key-0 reads), in key-tile loops and in epilogues, the block count,
+    // and the wave's first and last stamps: trace[(block * 4 + wave) * 8 + 0..5]
     constexpr bool TRACE = (VAR & 1024) != 0;
     unsigned long long tr_wait = 0, tr_loop = 0, tr_epi = 0, tr_n = 0, tr_t = 0;
     auto now = [&]() -> unsigned long long {
@@ -840,7 +840,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     bool stores_out = false;              // the previous block's 4 output stores may be in flight
     const f32x16 zero16 = {};
 
-    if constexpr (TRACE) tr_t = now();
+    unsigned long long tr_first = 0;
+    if constexpr (TRACE) tr_first = tr_t = now();
     for (int blk = blk_first; blk >= 0 && blk < nblk;) {
         // this block's Q, key-0 rows and K/V tile 0 landed (counted: the 4 stores after them may not)
         if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -1137,11 +1138,15 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     if constexpr (TRACE) {
         const long rec = (long)blockIdx.x * 4 + wave;
         if (trace && rec < trace_n && lane == 0) {
-            unsigned long long v[4] = {tr_wait, tr_loop, tr_epi, tr_n};
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            unsigned long long v[7] = {tr_wait, tr_loop, tr_epi, tr_n, tr_first, tr_t,
+                                       ((unsigned long long)xcc << 32) | hw};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 7; ++k) {
                 asm volatile("" : "+v"(v[k]));
-                trace[rec * 4 + k] = v[k];
+                trace[rec * 8 + k] = v[k];
             }
         }
     }
@@ -1300,7 +1305,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
     const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
-    const bool dyn = v == 4989 && (L - 1) / KBLK >= 3;
+    const bool dyn = (v == 4989 || v == 6013) && (L - 1) / KBLK >= 3;
     if (!causal && (v == 893 || v == 1917 || dyn) && clsk_ok && !lse && !seg) {
         // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
         static std::atomic<int> occ[kMaxDevices];
@@ -1328,8 +1333,12 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
                 if (e == hipSuccess) e = hipMemsetAsync(sc, 0, 64, s);
                 if (e != hipSuccess) return e;
             }
-            hipLaunchKernelGGL((attn_fwd_p<4989>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
-                               nullptr, 0, sc);
+            if (v == 6013)
+                hipLaunchKernelGGL((attn_fwd_p<6013>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
+                                   qscale, g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30), sc);
+            else
+                hipLaunchKernelGGL((attn_fwd_p<4989>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
+                                   qscale, nullptr, 0, sc);
             const hipError_t e = hipGetLastError();
             if (!sched) {
                 const hipError_t f = hipFreeAsync(sc, s);
@@ -1351,7 +1360,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v == 893 || v == 1917 || v == 4989) ? (clsk_ok ? 381 : 125)
+        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013) ? (clsk_ok ? 381 : 125)
                      : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
                      : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
@@ -1395,7 +1404,7 @@ int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
-                  var == 3453 || var == 1917 || var == 4989)
+                  var == 3453 || var == 1917 || var == 4989 || var == 6013)
                      ? var : 381;
     return prev;
 }

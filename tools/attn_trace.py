@@ -59,10 +59,24 @@ def main():
         _lib.call("ce_set_attn_trace", None, 0)
     finally:
         lib.ce_set_attn_variant(prev)
-    if args.var == 1917:
+    if args.var in (1917, 6013):
         # persistent kernel: per wave {time in block starts, key-tile loops, epilogues, blocks}
-        q = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+        q = buf.view(-1, 8).cpu().numpy().astype(np.int64)
         q = q[q[:, 3] > 0]
+        t0 = q[:, 4].min()
+        st, en = (q[:, 4] - t0) / 100.0, (q[:, 5] - t0) / 100.0
+        print(f"wave first stamp: p0 {st.min():.1f} p50 {np.percentile(st, 50):.1f} p90 {np.percentile(st, 90):.1f} "
+              f"max {st.max():.1f} us; last stamp: min {en.min():.1f} p50 {np.percentile(en, 50):.1f} "
+              f"p90 {np.percentile(en, 90):.1f} max {en.max():.1f} us")
+        xc = (q[:, 6] >> 32) & 0xf
+        allq = buf.view(-1, 8)[:, 3].cpu().numpy()
+        bid = np.nonzero(allq > 0)[0] // 4
+        for x in range(8):
+            m = xc == x
+            if m.any():
+                print(f"  XCC {x}: waves {int(m.sum())}, bid%8 == XCC {float(np.mean(bid[m] % 8 == x)):.2f}, "
+                      f"end p50 {np.percentile(en[m], 50):.1f} max {en[m].max():.1f} us, "
+                      f"loop per block {float(np.mean(q[m, 1] / 100.0 / q[m, 3])):.2f} us")
         nb = q[:, 3].astype(np.float64)
         print(f"persistent waves {len(q)}, blocks per wave {nb.mean():.2f} (min {nb.min():.0f}, max {nb.max():.0f})")
         for k, name in enumerate(("block_start", "loop", "epilogue")):
