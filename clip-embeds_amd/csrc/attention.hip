@@ -667,6 +667,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     // on one L2), then the other XCDs' ranges.  A workgroup learns its next block at the start of
     // the current one (wave 0, published through LDS at tile 1's barrier)
     constexpr bool DYN = (VAR & 4096) != 0;
+    // PRIO (bit 8192): the workgroups resident on a CU keep their dispatch order for the whole launch,
+    // and VALU issue goes to the oldest wave of a SIMD first, so in the static rounds the youngest
+    // workgroup of every CU is the slowest all the way (per-block loop times +-15 %);
+    // each block sets s_setprio (blocks done + workgroup slot on the CU) mod 3, rotating the order
+    constexpr bool PRIO = (VAR & 8192) != 0;
     // TRACE (bit 1024, diagnostics): per wave, the s_memrealtime time spent in block starts (the
     // counted wait + barrier + Q / key-0 reads), in key-tile loops and in epilogues, the block count,
     // and the wave's first and last stamps: trace[(block * 4 + wave) * 8 + 0..5]
@@ -840,9 +845,19 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     bool stores_out = false;              // the previous block's 4 output stores may be in flight
     const f32x16 zero16 = {};
 
+    unsigned prio_n = 0;
     unsigned long long tr_first = 0;
     if constexpr (TRACE) tr_first = tr_t = now();
     for (int blk = blk_first; blk >= 0 && blk < nblk;) {
+        if constexpr (PRIO) {
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            const int pr = (int)((prio_n + ((hw >> 16) & 0xf)) % 3);
+            if (pr == 0) __builtin_amdgcn_s_setprio(0);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(2);
+            ++prio_n;
+        }
         // this block's Q, key-0 rows and K/V tile 0 landed (counted: the 4 stores after them may not)
         if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1306,7 +1321,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     const int v = g_attn_var.load(std::memory_order_acquire);
     const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
     const bool dyn = (v == 4989 || v == 6013) && (L - 1) / KBLK >= 3;
-    if (!causal && (v == 893 || v == 1917 || dyn) && clsk_ok && !lse && !seg) {
+    if (!causal && (v == 893 || v == 1917 || v == 9085 || v == 10109 || dyn) && clsk_ok && !lse && !seg) {
         // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
         static std::atomic<int> occ[kMaxDevices];
         const int dev = current_device();
@@ -1349,6 +1364,11 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         if (v == 1917)
             hipLaunchKernelGGL((attn_fwd_p<1917>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
                                g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
+        else if (v == 10109)
+            hipLaunchKernelGGL((attn_fwd_p<10109>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
+                               g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
+        else if (v == 9085)
+            hipLaunchKernelGGL((attn_fwd_p<9085>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
         else
             hipLaunchKernelGGL((attn_fwd_p<893>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
         return hipGetLastError();
@@ -1360,7 +1380,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013) ? (clsk_ok ? 381 : 125)
+        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013 || v == 9085 || v == 10109) ? (clsk_ok ? 381 : 125)
                      : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
                      : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
@@ -1404,7 +1424,7 @@ int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
-                  var == 3453 || var == 1917 || var == 4989 || var == 6013)
+                  var == 3453 || var == 1917 || var == 4989 || var == 6013 || var == 9085 || var == 10109)
                      ? var : 381;
     return prev;
 }

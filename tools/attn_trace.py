@@ -59,7 +59,7 @@ def main():
         _lib.call("ce_set_attn_trace", None, 0)
     finally:
         lib.ce_set_attn_variant(prev)
-    if args.var in (1917, 6013):
+    if args.var in (1917, 6013, 10109):
         # persistent kernel: per wave {time in block starts, key-tile loops, epilogues, blocks}
         q = buf.view(-1, 8).cpu().numpy().astype(np.int64)
         q = q[q[:, 3] > 0]
