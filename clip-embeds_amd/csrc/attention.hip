@@ -1320,7 +1320,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
     const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
-    const bool dyn = (v == 4989 || v == 6013) && (L - 1) / KBLK >= 3;
+    const bool dyn = (v == 4989 || v == 6013 || v == 13181) && (L - 1) / KBLK >= 3;
     if (!causal && (v == 893 || v == 1917 || v == 9085 || v == 10109 || dyn) && clsk_ok && !lse && !seg) {
         // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
         static std::atomic<int> occ[kMaxDevices];
@@ -1351,6 +1351,9 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
             if (v == 6013)
                 hipLaunchKernelGGL((attn_fwd_p<6013>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
                                    qscale, g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30), sc);
+            else if (v == 13181)
+                hipLaunchKernelGGL((attn_fwd_p<13181>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
+                                   qscale, nullptr, 0, sc);
             else
                 hipLaunchKernelGGL((attn_fwd_p<4989>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
                                    qscale, nullptr, 0, sc);
@@ -1380,7 +1383,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013 || v == 9085 || v == 10109) ? (clsk_ok ? 381 : 125)
+        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013 || v == 9085 || v == 10109 || v == 13181) ? (clsk_ok ? 381 : 125)
                      : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
                      : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
@@ -1424,7 +1427,7 @@ int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
-                  var == 3453 || var == 1917 || var == 4989 || var == 6013 || var == 9085 || var == 10109)
+                  var == 3453 || var == 1917 || var == 4989 || var == 6013 || var == 9085 || var == 10109 || var == 13181)
                      ? var : 381;
     return prev;
 }
