@@ -152,6 +152,10 @@ def lib():
                 "(or __graft_entry__.build()); there is no CPU fallback")
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
+            # an explicitly chosen older build (CLIPEMBED_LIB, same-box A/B of two builds) may predate a
+            # few diagnostic / A/B entry points: those stay unbound; the default library must export all
+            if os.environ.get("CLIPEMBED_LIB") and not hasattr(handle, name):
+                continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -156,6 +156,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int qrow = qb * QBLK + wave * 32 + r;
     const int q_wave0 = qb * QBLK + wave * 32;        // first query of this wave (wave-uniform)
 
+    // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
+    bf16x8 qf[4];
+    if constexpr (!EARLY) {
+        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+        // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
+        // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
+        if (qscale != 1.0f) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
+        }
+    }
+
     // staging: thread -> row tid>>3 of a 32-row pass, 16-B chunk tid&7
     const int srow = tid >> 3;
     const int spos = tid & 7;
@@ -214,9 +230,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
             if (nkt > 1) stage(1, 1);
         }
     }
-    // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
-    bf16x8 qf[4];
-    {
+    if constexpr (EARLY) {
         const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
@@ -234,9 +248,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
             for (int g = 0; g < 4; ++g) v0w[dt][g] = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
     }
-    // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
-    // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
-    if (qscale != 1.0f) {
+    if (EARLY && qscale != 1.0f) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -292,13 +304,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const bf16x8 kv = EARLY ? k0v[ks] : *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
-            // v_dot2_f32_bf16 on the bf16 pairs: 16 instructions instead of 32 FMAs + 64 unpacks
+            // (f32 FMAs: v_dot2_f32_bf16 here, with the packed multiplies below, took the kernel to 126
+            // VGPRs and four waves per SIMD, 1 % slower than three in a same-box A/B)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const bf16x2_t qa = {qf[ks][2 * e], qf[ks][2 * e + 1]};
-                const bf16x2_t ka = {kv[2 * e], kv[2 * e + 1]};
-                a = __builtin_amdgcn_fdot2_f32_bf16(qa, ka, a, false);
-            }
+            for (int e = 0; e < 8; ++e) a = fmaf((float)qf[ks][e], (float)kv[e], a);
         }
         s0v = a + __shfl_xor(a, 32, 64);
         fix_ok = MODE >= 1 && __all(s0v <= 64.0f && s0v >= -64.0f);
@@ -312,11 +321,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const uint2 w = EARLY ? v0w[dt][g] : *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
-                const f32x2 pp = {p0, p0};
-                const f32x2 x0 = f32x2{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u)} * pp;
-                const f32x2 x1 = f32x2{__uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)} * pp;
-                o[dt][4 * g + 0] = x0.x; o[dt][4 * g + 1] = x0.y;
-                o[dt][4 * g + 2] = x1.x; o[dt][4 * g + 3] = x1.y;
+                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
+                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
+                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
+                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
             }
     }
 
@@ -612,14 +620,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #pragma unroll
             for (int gp = 0; gp < 2; ++gp) {
                 const int g0 = 2 * gp, g1 = 2 * gp + 1;
-                // (v_pk_mul_f32: no MFMAs to sit beside here)
-                const f32x2 iv = {inv, inv};
-                const f32x2 a0 = f32x2{o[dt][4 * g0 + 0], o[dt][4 * g0 + 1]} * iv;
-                const f32x2 a1 = f32x2{o[dt][4 * g0 + 2], o[dt][4 * g0 + 3]} * iv;
-                const f32x2 b0 = f32x2{o[dt][4 * g1 + 0], o[dt][4 * g1 + 1]} * iv;
-                const f32x2 b1 = f32x2{o[dt][4 * g1 + 2], o[dt][4 * g1 + 3]} * iv;
-                const uint32_t ax = pack_bf2(a0.x, a0.y), ay = pack_bf2(a1.x, a1.y);
-                const uint32_t bx = pack_bf2(b0.x, b0.y), by = pack_bf2(b1.x, b1.y);
+                const uint32_t ax = pack_bf2(o[dt][4 * g0 + 0] * inv, o[dt][4 * g0 + 1] * inv);
+                const uint32_t ay = pack_bf2(o[dt][4 * g0 + 2] * inv, o[dt][4 * g0 + 3] * inv);
+                const uint32_t bx = pack_bf2(o[dt][4 * g1 + 0] * inv, o[dt][4 * g1 + 1] * inv);
+                const uint32_t by = pack_bf2(o[dt][4 * g1 + 2] * inv, o[dt][4 * g1 + 3] * inv);
                 const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
                 const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
                 if (qrow < L)
