@@ -41,7 +41,7 @@ def test_attention_persistent(B, L, H, scale):
         # the blocks' arithmetic does not depend on which workgroup runs them: bitwise equal to the
         # static rounds and from launch to launch (the counters reset themselves)
         assert torch.equal(out, run_var(var, qkv, B, L, H)), var
-        if var == 4989:
+        if var == 4989 and (L - 1) // 64 >= 3:      # (fewer key tiles: 4989 runs variant 381)
             assert torch.equal(out, run_var(893, qkv, B, L, H))
 
 
