@@ -662,15 +662,7 @@ template <int VAR>
 __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                      int L, int H, int nblk, float qscale,
                                                      unsigned long long* __restrict__ trace = nullptr,
-                                                     int trace_n = 0, int* __restrict__ sched = nullptr) {
-    // DYN (bit 4096): blocks handed out at run time from per-XCD counters (sched[0..7]; sched[8]
-    // counts finished workgroups, and the last one resets all nine to 0 for the next launch) instead
-    // of the static rounds: a static assignment runs as long as its slowest CU, and per-wave block
-    // times spread by +-15 % (tools/attn_trace.py --var 1917: the waves' mean 403 us against a 513-us
-    // launch).  XCD x serves blocks [x nblk / 8, (x + 1) nblk / 8) first (the q-blocks of a head stay
-    // on one L2), then the other XCDs' ranges.  A workgroup learns its next block at the start of
-    // the current one (wave 0, published through LDS at tile 1's barrier)
-    constexpr bool DYN = (VAR & 4096) != 0;
+                                                     int trace_n = 0) {
     // PRIO (bit 8192): the workgroups resident on a CU keep their dispatch order for the whole launch,
     // and VALU issue goes to the oldest wave of a SIMD first, so in the static rounds the youngest
     // workgroup of every CU is the slowest all the way (per-block loop times +-15 %);
@@ -691,8 +683,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     };
     constexpr int QOFF = 2 * STAGE_BYTES;
     constexpr int COFF = QOFF + QBLK * 128;
-    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024 + 16];
-    int* const s_next = reinterpret_cast<int*>(smem + COFF + 1024);
+    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024];
     // blocks slot, slot + G, slot + 2G, ...: the grid walks the blocks in rounds, and slot is the XCD-aware
     // remap of attn_fwd, so the q-blocks of one (batch, head) run at the same time on one XCD and
     // share its K / V tiles in that XCD's L2 (contiguous runs per workgroup re-read every head's K / V
@@ -700,53 +691,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     const int G = gridDim.x;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qn = G >> 3, rn = G & 7;
-    // wave 0, lane 0: the next block from the counters (-1: none left), written to s_next.  Split so
-    // the common case's atomic has a key tile to return: grab_issue (own XCD's counter) at a block's
-    // start, grab_finish at the end of its tile 0 (the other XCDs' counters, in turn, only once the own
-    // range is used up)
-    const int own_lo = (int)((long)xcd * nblk / 8), own_hi = (int)((long)(xcd + 1) * nblk / 8);
-    // The block-start atomic's result is consumed by every lane (lanes other than 0 hold the "no block"
-    // value): a use on lane 0's path only would leave the atomic pending, for the compiler's wait
-    // analysis, on the path that skips it, and hipcc then waits for it (and, in vmcnt's issue order,
-    // for the previous block's output stores) at the loop head.  (Inline asm instead lets hipcc copy
-    // the result register before the atomic has written it: blocks were lost.)
-    auto grab_issue = [&](int& dyn_k) __attribute__((always_inline)) {
-        if constexpr (DYN) {
-            dyn_k = 1 << 30;
-            if (threadIdx.x == 0 && own_lo < own_hi) dyn_k = atomicAdd(&sched[xcd], 1);
-        }
-    };
-    auto grab_finish = [&](int dyn_k) __attribute__((always_inline)) {
-        if constexpr (DYN) {
-            int got = dyn_k < own_hi - own_lo ? own_lo + dyn_k : -1;
-            if (threadIdx.x == 0) {
-                for (int j = 1; j < 8 && got < 0; ++j) {
-                    const int x = (xcd + j) & 7;
-                    const int lo = (int)((long)x * nblk / 8), hi = (int)((long)(x + 1) * nblk / 8);
-                    if (lo >= hi) continue;
-                    const int kk = atomicAdd(&sched[x], 1);
-                    if (lo + kk < hi) got = lo + kk;
-                }
-                *s_next = got;
-            }
-        }
-    };
-    int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
-    if constexpr (DYN) {
-        int k0 = 0;
-        grab_issue(k0);
-        grab_finish(k0);
-        barrier();
-        blk_first = *s_next;
-        barrier();                        // (every wave read it before wave 0's next grab overwrites it)
-        if (blk_first < 0) {
-            if (threadIdx.x == 0 && atomicAdd(&sched[8], 1) == G - 1)
-                for (int i = 0; i < 9; ++i) sched[i] = 0;
-            return;                       // workgroup-uniform
-        }
-    } else {
-        if (blk_first >= nblk) return;    // workgroup-uniform
-    }
+    const int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    if (blk_first >= nblk) return;        // workgroup-uniform
     const int nqb = (L + QBLK - 1) / QBLK;
     const int D = H * 64;
     const int ld2 = 6 * D;                // bytes per qkv row
@@ -852,7 +798,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
     unsigned prio_n = 0;
     unsigned long long tr_first = 0;
     if constexpr (TRACE) tr_first = tr_t = now();
-    for (int blk = blk_first; blk >= 0 && blk < nblk;) {
+    for (int blk = blk_first; blk < nblk; blk += G) {
         if constexpr (PRIO) {
             unsigned hw;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -866,26 +812,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
         if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier();
-        // next block: static rounds, or (DYN) grabbed now (the atomic returns under tile 0; wave 0
-        // publishes it at the end of tile 0 and every wave reads it after tile 1's barrier)
-        int dyn_k = 0;
-        if constexpr (DYN) grab_issue(dyn_k);
-        int nblk_id = blk + G;
-        bool has_next = !DYN && nblk_id < nblk;
-        Blk nxt = decode(has_next ? nblk_id : blk);
-        __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
-        __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
-        __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
-        auto learn_next = [&]() __attribute__((always_inline)) {
-            if constexpr (DYN) {
-                nblk_id = __builtin_amdgcn_readfirstlane(*s_next);
-                has_next = nblk_id >= 0;
-                nxt = decode(has_next ? nblk_id : blk);
-                nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
-                nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
-                nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
-            }
-        };
+        const int nblk_id = blk + G;
+        const bool has_next = nblk_id < nblk;
+        const Blk nxt = decode(has_next ? nblk_id : blk);
+        const __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
+        const __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
+        const __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
         const int q_wave0 = cur.qb * QBLK + wave * 32;
         const int qrow = q_wave0 + r;
         const bool active = q_wave0 < L;  // wave-uniform
@@ -992,7 +924,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
             // every wave has read this block's Q by tile 1's barrier), behind that tile's K / V DMAs, so
             // tile qt + 1 waits for its own K / V only (counted: the Q pieces issued after them stay in
             // flight) and they have two tiles to land; with fewer tiles, at the last tile
-            const int qt = nkt >= 3 ? 1 : nkt - 1;      // (DYN: nkt >= 3, launcher)
+            const int qt = nkt >= 3 ? 1 : nkt - 1;
             if (t > 0 || nkt == 1) {
                 if (t == qt + 1 && has_next) {
                     if (wave == 0) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
@@ -1002,7 +934,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
                 }
                 barrier();
             }
-            if (DYN && t == 1) learn_next();      // (wave 0 wrote s_next before this barrier: grab_finish)
             if (t + 1 < nkt) {
                 stage_kv(t + 1, std::integral_constant<int, BUF ^ 1>{}, ksrd, vsrd);
             } else if (has_next) {
@@ -1089,9 +1020,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
                 l_run += psum;
                 pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
             }
-            if constexpr (DYN) {
-                if (t == 0) grab_finish(dyn_k);
-            }
         };
         auto run = [&](auto pc) __attribute__((always_inline)) {
             constexpr int P = decltype(pc)::value;
@@ -1107,9 +1035,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
         }
         if (par) run(std::integral_constant<int, 1>{});
         else run(std::integral_constant<int, 0>{});
-        // (a use of the block-start atomic's result on every path, so the compiler's wait analysis
-        // never carries it pending round the loop: it would wait for it at the loop head)
-        if constexpr (DYN) asm volatile("" : : "v"(dyn_k));
         if constexpr (TRACE) {
             tr_t = now();
             tr_loop += tr_t - tl0;
@@ -1147,12 +1072,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ 
         cur = nxt;
         qsrd = nqsrd; ksrd = nksrd; vsrd = nvsrd;
         par ^= nkt & 1;
-        blk = has_next ? nblk_id : -1;
-    }
-    if constexpr (DYN) {
-        // the last workgroup out resets the counters (every other one has finished its grabs)
-        if (threadIdx.x == 0 && atomicAdd(&sched[8], 1) == G - 1)
-            for (int i = 0; i < 9; ++i) sched[i] = 0;
     }
     if constexpr (TRACE) {
         const long rec = (long)blockIdx.x * 4 + wave;
@@ -1316,7 +1235,7 @@ hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* ou
 }
 
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
-                            hipStream_t s, float* lse, const int* seg, int* sched) {
+                            hipStream_t s, float* lse, const int* seg) {
     if (B <= 0 || L <= 0) return hipSuccess;
     const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
@@ -1324,8 +1243,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
     const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
-    const bool dyn = (v == 4989 || v == 6013 || v == 13181) && (L - 1) / KBLK >= 3;
-    if (!causal && (v == 893 || v == 1917 || v == 9085 || v == 10109 || dyn) && clsk_ok && !lse && !seg) {
+    if (!causal && (v == 893 || v == 1917 || v == 9085 || v == 10109) && clsk_ok && !lse && !seg) {
         // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
         static std::atomic<int> occ[kMaxDevices];
         const int dev = current_device();
@@ -1344,30 +1262,6 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         const long nblk = (long)((L + QBLK - 1) / QBLK) * H * B;
         if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
         const int g = (int)std::min<long>(nblk, (long)per_cu * device_cus());
-        if (dyn) {
-            // the caller's 9 zeroed ints (left zeroed by the kernel), or a stream-ordered temporary
-            int* sc = sched;
-            if (!sc) {
-                hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&sc), 64, s);
-                if (e == hipSuccess) e = hipMemsetAsync(sc, 0, 64, s);
-                if (e != hipSuccess) return e;
-            }
-            if (v == 6013)
-                hipLaunchKernelGGL((attn_fwd_p<6013>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
-                                   qscale, g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30), sc);
-            else if (v == 13181)
-                hipLaunchKernelGGL((attn_fwd_p<13181>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
-                                   qscale, nullptr, 0, sc);
-            else
-                hipLaunchKernelGGL((attn_fwd_p<4989>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk,
-                                   qscale, nullptr, 0, sc);
-            const hipError_t e = hipGetLastError();
-            if (!sched) {
-                const hipError_t f = hipFreeAsync(sc, s);
-                if (e == hipSuccess && f != hipSuccess) return f;
-            }
-            return e;
-        }
         if (v == 1917)
             hipLaunchKernelGGL((attn_fwd_p<1917>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
                                g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
@@ -1387,7 +1281,7 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
         else CE_ATTN_LAUNCH(true, 0);
     } else {
         // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v == 893 || v == 1917 || v == 4989 || v == 6013 || v == 9085 || v == 10109 || v == 13181) ? (clsk_ok ? 381 : 125)
+        const int vv = (v == 893 || v == 1917 || v == 9085 || v == 10109) ? (clsk_ok ? 381 : 125)
                      : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
                      : (v & 256) && !clsk_ok ? (v & ~256) : v;
         switch (vv) {
@@ -1431,7 +1325,7 @@ int set_attn_variant(int var) {
     const int prev = g_attn_var.load();
     g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
                   var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
-                  var == 3453 || var == 1917 || var == 4989 || var == 6013 || var == 9085 || var == 10109 || var == 13181)
+                  var == 3453 || var == 1917 || var == 9085 || var == 10109)
                      ? var : 381;
     return prev;
 }

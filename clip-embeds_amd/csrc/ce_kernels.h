@@ -134,9 +134,7 @@ void set_attn_trace(unsigned long long* buf, long n);   // diagnostics: per-wave
 int set_fgemm_variant(int v);   // 1 = register-blocked f32 GEMM (default), 0 = the 64 x 64 kernel
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse = nullptr,   // lse: [B][H][L] log2 log-sum-exp (training)
-                            const int* seg = nullptr,
-                            int* sched = nullptr);   // 9 zeroed ints the dynamic persistent variant hands blocks out from
-                                                     // (left zeroed; nullptr: a stream-ordered temporary per launch)  // seg: packed sequences (launch_text_pack), L = max length
+                            const int* seg = nullptr);  // seg: packed sequences (launch_text_pack), L = max length
 // The same attention for ONE query row per sequence (row qrows[b], absolute; null: row b*L), keys
 // of sequence b only (0..qrows[b]-b*L with causal); out [B][D] bf16 compact.  q pre-scaled as
 // launch_attention(q_prescaled).  src/dst (optional): copy the selected rows of the hi/lo planes

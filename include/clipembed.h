@@ -325,10 +325,8 @@ int ce_set_gemm_variant(int bits);
  * Round-5 measurement variants of the non-causal (L - 1) % 64 == 0 launch (other
  * launches run 381 / 125): 2429 = 381 with tile 0's DMA and every prologue load issued at entry; 893 =
  * a persistent grid (3 workgroups per CU walking the q-blocks in rounds, the next block's Q / key-0 rows /
- * tile 0 DMA'd during the current block); 4989 = 893 with the blocks handed out at run time from
- * per-XCD counters (>= 3 key tiles; the raw kernel entry allocates the counters per launch); 9085 = 893
- * with a per-block rotating s_setprio; 13181 = 4989 + that rotation; 1405 / 1917 / 6013 / 10109 = 381 /
- * 893 / 4989 / 9085 recording timelines through ce_set_attn_trace.  All measured slower than 381.
+ * tile 0 DMA'd during the current block); 9085 = 893 with a per-block rotating s_setprio; 1405 / 1917 /
+ * 10109 = 381 / 893 / 9085 recording timelines through ce_set_attn_trace.  All measured slower than 381.
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 3 = the

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--L", type=int, default=577)
     ap.add_argument("--H", type=int, default=16)
-    ap.add_argument("--var", type=int, default=1405, help="1405 (381 + stamps), 3453 (2429 + stamps), 1917 (893 + phase sums)")
+    ap.add_argument("--var", type=int, default=1405, help="1405 (381 + stamps), 3453 (2429 + stamps), 1917 / 10109 (893 / 9085 + phase sums)")
     args = ap.parse_args()
     B, L, H = args.batch, args.L, args.H
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -59,7 +59,7 @@ def main():
         _lib.call("ce_set_attn_trace", None, 0)
     finally:
         lib.ce_set_attn_variant(prev)
-    if args.var in (1917, 6013, 10109):
+    if args.var in (1917, 10109):
         # persistent kernel: per wave {time in block starts, key-tile loops, epilogues, blocks}
         q = buf.view(-1, 8).cpu().numpy().astype(np.int64)
         q = q[q[:, 3] > 0]
