@@ -112,7 +112,6 @@ _SIGNATURES = {
     "ce_set_train_dw_tn": (c_int, [c_int]),
     "ce_set_train_act_bwd_fuse": (c_int, [c_int]),
     "ce_set_gemm_trace": (c_int, [c_void_p, c_int64]),
-    "ce_set_attn_trace": (c_int, [c_void_p, c_int64]),
     "ce_gemm_path_counts": (c_int, [POINTER(c_int64), c_int, c_int]),
     "ce_set_gemm_schedule": (c_int, [c_int]),
     "ce_set_gemm_splitk": (c_int, [c_int]),

@@ -66,65 +66,32 @@ __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
 }
 
-// Variants (set_attn_variant): 0 = every tile on the general online-softmax path;
-// 1 = "fixed-offset" tiles: once tile 0 has shown every row max of the wave within +-64 (log2
-// units), the softmax offset stays 0 and full tiles skip the row max, the accumulator moves and
-// the subtraction (p = exp2(q.k) directly; bf16 P has the f32 exponent range, O and l the same
-// factor), with an overflow check on the row sums (any p > 2^64 or inf/NaN: the tile is redone
-// with the exact max and the wave returns to the general path); 2 = as 1, with the row sums of
-// the fast tiles taken by the MFMA (a ones A operand beside the P.V products: l^T = 1 P^T) and
-// the overflow check on a max3 reduction of the scores.
+// Variants (the VAR bits; set_attn_variant selects among the instantiated ones, DESIGN.md §6.6,
+// §6.9, §6.12): MODE (bits 0-1) 0 = every tile on the general online-softmax path; 1 = "fixed-offset"
+// tiles: once tile 0 has shown every row max of the wave within +-64 (log2 units), the softmax offset
+// stays 0 and full tiles skip the row max, the accumulator moves and the subtraction (p = exp2(q.k)
+// directly; bf16 P has the f32 exponent range, O and l the same factor), with an overflow check on
+// the row sums (any p > 2^64 or inf/NaN: the tile is redone with the exact max and the wave returns
+// to the general path).  Every instantiation has the 16-B output stores (bit 8), the inline-asm V^T
+// reads (bit 16) and the buffer-descriptor K/V DMAs (bit 64).  Instantiated: 381 (non-causal
+// L = 64k + 1, default), 125 (non-causal, other L), 88 (causal).  (Measured and removed in round 6:
+// MFMA row sums, a three-slot ring, early prologue loads, per-wave timelines and the persistent
+// variants)
 template <bool CAUSAL, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int Lp, int H,
                                                     float qscale, float* __restrict__ lse,
-                                                    const int* __restrict__ seg,
-                                                    unsigned long long* __restrict__ trace = nullptr,
-                                                    int trace_n = 0) {
-    constexpr bool RING3 = (VAR & 128) != 0;  // three K/V slots: tile t+2 in flight beside t+1 (ONEBAR)
-    __shared__ __attribute__((aligned(16))) char smem[(RING3 ? 3 : 2) * STAGE_BYTES];
-    constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset, 2 + MFMA row sums
+                                                    const int* __restrict__ seg) {
+    static_assert((VAR & (8 | 16 | 64)) == (8 | 16 | 64) && (VAR & 3) <= 1, "attn_fwd: instantiated variant set");
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
-    constexpr bool WIDE = (VAR & 8) != 0;    // 16-B output stores (lane pairs l, l^32 trade halves)
-    constexpr bool ASMV = (VAR & 16) != 0;   // V^T reads by inline asm (no vmcnt(0) before P.V)
     constexpr bool FAST0 = (VAR & 32) != 0;  // tile 0 on the fixed offset too (two-sided check)
-    constexpr bool BUFDMA = (VAR & 64) != 0; // K/V DMAs through clipped buffer descriptors
     // CLSK (bit 256, non-causal, (L - 1) % 64 == 0): key 0 (the CLS token) enters the softmax up
     // front (one 64-d dot product per query on the VALU, O and l initialised with its term) and the
     // key tiles cover keys 1..L-1: L = 577 runs 9 full tiles instead of 9 + one single-key tile on the
     // masked general path
     constexpr bool CLSK = !CAUSAL && (VAR & 256) != 0;
-    constexpr bool EARLY = (VAR & 2048) != 0;
-    // TRACE (bit 1024, diagnostics, ce_set_attn_trace): lane 0 of every wave records s_memrealtime
-    // (100 MHz) at entry, after the prologue (Q, key 0), after tile 0's wait, after the tile loop and
-    // after the stores, plus (XCC id << 32 | HW_ID), into its own 8-word record (vector stores)
-    constexpr bool TRACE = (VAR & 1024) != 0;
-    unsigned long long* trec = nullptr;
-    if constexpr (TRACE) {
-        const long rec = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (trace && rec < trace_n) trec = trace + rec * 8;
-    }
-    auto stamp = [&](int slot) {
-        if constexpr (TRACE) {
-            if (trec && (threadIdx.x & 63) == 0) {
-                unsigned long long t = __builtin_amdgcn_s_memrealtime();
-                asm volatile("" : "+v"(t));
-                trec[slot] = t;
-            }
-        }
-    };
-    stamp(0);
-    if constexpr (TRACE) {
-        if (trec && (threadIdx.x & 63) == 0) {
-            unsigned hw, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            unsigned long long id = ((unsigned long long)xcc << 32) | hw;
-            asm volatile("" : "+v"(id));
-            trec[5] = id;
-        }
-    }
-
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
     const int nqb = (Lp + QBLK - 1) / QBLK;
@@ -158,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 
     // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
     bf16x8 qf[4];
-    if constexpr (!EARLY) {
+    {
         const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
@@ -183,77 +150,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const bf16_t* kbase = base + D + h * 64 + (CLSK ? ld : 0);
     const bf16_t* vbase = base + 2 * D + h * 64 + (CLSK ? ld : 0);
 
-    // BUFDMA: the K / V columns of this (b, h) as buffer descriptors clipped after row L - 1 (rows
-    // past the end read zeros: masked keys), per-lane row/chunk offsets computed once, the tile's
-    // row offset one scalar add per DMA (the flat form rebuilt 64-bit addresses with 64-bit
-    // multiplies for every DMA)
+    // the K / V columns of this (b, h) as buffer descriptors clipped after row L - 1 (rows past the
+    // end read zeros: masked keys), per-lane row/chunk offsets computed once, the tile's row offset
+    // one scalar add per DMA (the flat form rebuilt 64-bit addresses with 64-bit multiplies for
+    // every DMA)
     const int ld2 = (int)ld * 2;
-    const int nrec = BUFDMA ? (Lk - 1) * ld2 + 128 : 0;
+    const int nrec = (Lk - 1) * ld2 + 128;
     const __amdgpu_buffer_rsrc_t ksrd = attn_srd(kbase, nrec);
     const __amdgpu_buffer_rsrc_t vsrd = attn_srd(vbase, nrec);
-    int kvo[2] = {0, 0}, vvo[2] = {0, 0};
-    if constexpr (BUFDMA) {
+    int kvo[2], vvo[2];
 #pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-            kvo[ps] = (ps * 32 + srow) * ld2 + kchunk * 16;
-            vvo[ps] = (ps * 32 + srow) * ld2 + vchunk * 16;
-        }
+    for (int ps = 0; ps < 2; ++ps) {
+        kvo[ps] = (ps * 32 + srow) * ld2 + kchunk * 16;
+        vvo[ps] = (ps * 32 + srow) * ld2 + vchunk * 16;
     }
     auto stage = [&](int t, int buf) {
         char* dst = smem + buf * STAGE_BYTES + wave * 1024;
-        if constexpr (BUFDMA) {
-            const int ro = t * KBLK * ld2;
-#pragma unroll
-            for (int ps = 0; ps < 2; ++ps) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (CE_LDS void*)(dst + ps * 4096), 16, kvo[ps] + ro, 0, 0, 0);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (CE_LDS void*)(dst + TILE_KV_BYTES + ps * 4096), 16,
-                                                         vvo[ps] + ro, 0, 0, 0);
-            }
-            return;
-        }
+        const int ro = t * KBLK * ld2;
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
-            const int key = min(t * KBLK + ps * 32 + srow, Lk - 1);
-            glds16(kbase + (size_t)key * ld + kchunk * 8, dst + ps * 4096);
-            glds16(vbase + (size_t)key * ld + vchunk * 8, dst + TILE_KV_BYTES + ps * 4096);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (CE_LDS void*)(dst + ps * 4096), 16, kvo[ps] + ro, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (CE_LDS void*)(dst + TILE_KV_BYTES + ps * 4096), 16,
+                                                     vvo[ps] + ro, 0, 0, 0);
         }
     };
-
-    // EARLY (bit 2048): tile 0's K / V DMA goes out before the Q and key-0 loads, and those loads are
-    // all issued before the first use of any of them, so the wave waits for one memory latency at
-    // entry instead of three in a row (Q, then key 0, then tile 0: tools/attn_trace.py measured
-    // 4.6 us of prologue + 2.7 us of tile-0 wait per 32-query wave against 15 us of key tiles at
-    // L = 577)
-    if constexpr (EARLY) {
-        stage(0, 0);
-        if constexpr (RING3) {
-            if (nkt > 1) stage(1, 1);
-        }
-    }
-    if constexpr (EARLY) {
-        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-    }
-    // key 0's K row (CLSK) and V row words, loaded with Q (EARLY) so their latencies overlap
-    bf16x8 k0v[4];
-    uint2 v0w[2][4];
-    if constexpr (CLSK && EARLY) {
-        const bf16_t* k0 = base + D + h * 64 + 8 * h2;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) k0v[ks] = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
-        const bf16_t* v0 = base + 2 * D + h * 64;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) v0w[dt][g] = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
-    }
-    if (EARLY && qscale != 1.0f) {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
-    }
 
     // per-lane LDS read offsets
     int koff[2][4];
@@ -279,14 +199,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     f32x16 o[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-    // VAR 2: row sums of the fast tiles, l^T = 1 . P^T (every entry of a lane = its query's sum
-    // over both key halves; entry 0 is read)
-    f32x16 lm;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) lm[i] = 0.f;
-    bf16x8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
     float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
     float l_run = 0.f;   // partial (this half's keys)
     // wave-uniform: softmax offset fixed at 0 (MODE >= 1).  FAST0 (bit 32): tile 0 too starts on the
@@ -303,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         float a = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-            const bf16x8 kv = EARLY ? k0v[ks] : *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+            const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
             // (f32 FMAs: v_dot2_f32_bf16 here, with the packed multiplies below, took the kernel to 126
             // VGPRs and four waves per SIMD, 1 % slower than three in a same-box A/B)
 #pragma unroll
@@ -320,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const uint2 w = EARLY ? v0w[dt][g] : *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
+                const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
                 o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
                 o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
                 o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
@@ -371,61 +283,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
 #undef CE_TRV
     };
 
-    // O^T += V^T P^T for the tile's P fragments (pf[kt2][s2]: keys kt2*32 + 16*s2 .. +15)
-    auto pv = [&](const char* vb, const bf16x8 (&pf)[2][2], bool with_half2, bool rowsum) {
-#pragma unroll
-        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                if (kt2 == 1 && !with_half2) continue;
-                const int krow = kt2 * 32 + 16 * s2;
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const char* a0 = vb + krow * 128 + voff[dt];
-                    const s16x4 lo = ds_read_tr16(a0);
-                    const s16x4 hi = ds_read_tr16(a0 + 8 * 128);
-                    typedef __attribute__((ext_vector_type(8))) short s16x8;
-                    const s16x8 v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                    const bf16x8 vf = __builtin_bit_cast(bf16x8, v8);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt2][s2], o[dt], 0, 0, 0);
-                }
-                if (rowsum) lm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kt2][s2], lm, 0, 0, 0);
-            }
-    };
     // rescale of O and l by 2^-delta (delta per lane, equal on lanes l and l^32)
     auto rescale = [&](float delta) {
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         l_run *= alpha;
-        lm[0] *= alpha;
 #pragma unroll
         for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
         m_run += delta;
     };
 
-    stamp(1);
-    if constexpr (!EARLY) {
-        stage(0, 0);
-        if constexpr (RING3) {
-            if (nkt > 1) stage(1, 1);
-        }
-    }
-    // one key tile; BUF (the ring slot, t & 1, or t % 3 with RING3) is a compile-time constant so
-    // every LDS address is a per-lane offset plus an immediate (the loop is unrolled by two / three)
+    stage(0, 0);
+    // one key tile; BUF (the ring slot, t & 1) is a compile-time constant so every LDS address is a
+    // per-lane offset plus an immediate (the loop is unrolled by two)
     auto tile = [&](const int t, auto bufc) {
         constexpr int BUF = decltype(bufc)::value;
-        if constexpr (RING3) {
-            // tile t landed (tile t+1's 4 DMAs may stay in flight) and every wave is done with tile
-            // t-1, whose slot (t+2) % 3 then takes tile t+2
-            if (t + 1 < nkt) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            barrier();
-            if (t + 2 < nkt) stage(t + 2, (BUF + 2) % 3);
-        } else if (ONEBAR) {
+        if (ONEBAR) {
             // tile t landed (the only DMA in flight) and every wave is done with tile t-1, whose
             // slot BUF^1 then takes tile t+1
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             barrier();
-            if (t == 0) stamp(2);
             if (t + 1 < nkt) stage(t + 1, BUF ^ 1);
         } else {
             if (t + 1 < nkt) {
@@ -460,53 +336,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                     const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
                     s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? zero16 : s[kt2], 0, 0, 0);
                 }
-            bool overflow;
-            float psum = 0.f;
+            float ps[4] = {0.f, 0.f, 0.f, 0.f};
             bf16x8 pf[2][2];
-            if (MODE == 2) {
-                // overflow check on the scores themselves (the sums come from the MFMA)
-                float mx[2];
 #pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2) {
-                    float a = s[kt2][0];
+            for (int kt2 = 0; kt2 < 2; ++kt2)
 #pragma unroll
-                    for (int i = 1; i < 16; i += 2) a = fmaxf(a, fmaxf(s[kt2][i], s[kt2][i + 1]));
-                    mx[kt2] = a;
-                }
-                // !(x <= 64) also catches NaN
-                overflow = __any(!(fmaxf(mx[0], mx[1]) <= 64.0f));
-            } else {
-                float ps[4] = {0.f, 0.f, 0.f, 0.f};
+                for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
-                            ps[j & 3] += pv_;
-                            pf[kt2][s2][j] = (__bf16)pv_;
-                        }
-                psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-                overflow = __any(!(psum <= 0x1p64f)) || (FAST0 && t == 0 && __any(!(psum >= 0x1p-64f)));
-            }
+                    for (int j = 0; j < 8; ++j) {
+                        const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                        ps[j & 3] += pv_;
+                        pf[kt2][s2][j] = (__bf16)pv_;
+                    }
+            const float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+            // (!(x <= 2^64) also catches NaN)
+            const bool overflow = __any(!(psum <= 0x1p64f)) || (FAST0 && t == 0 && __any(!(psum >= 0x1p-64f)));
             if (!overflow) {
-                if (MODE == 2) {
-#pragma unroll
-                    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                            for (int j = 0; j < 8; ++j)
-                                pf[kt2][s2][j] = (__bf16)__builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
-                } else {
-                    l_run += psum;
-                }
+                l_run += psum;
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (ASMV && MODE != 2)
-                    pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, true);
-                else
-                    pv(vb, pf, true, MODE == 2);
+                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, true);
             } else {
                 // rare: the tile is redone on the general path below (exact row max, rescale),
                 // and the wave stays there
@@ -581,38 +429,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                         pf[kt2][s2][j] = (__bf16)pv_;
                     }
             l_run += psum;
-            if constexpr (ASMV)
-                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, half2);
-            else
-                pv(vb, pf, half2, false);
+            pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, half2);
         }
         if (!ONEBAR) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             barrier();
         }
     };
-    if constexpr (RING3) {
-        for (int t = 0; t < nkt; t += 3) {
-            tile(t, std::integral_constant<int, 0>{});
-            if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
-            if (t + 2 < nkt) tile(t + 2, std::integral_constant<int, 2>{});
-        }
-    } else {
-        for (int t = 0; t < nkt; t += 2) {
-            tile(t, std::integral_constant<int, 0>{});
-            if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
-        }
+    for (int t = 0; t < nkt; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
     }
 
-    stamp(3);
     // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64) + (MODE == 2 ? lm[0] : 0.f);
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
     const float inv = 1.0f / l_tot;
     // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
     if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * Lp + qrow] = m_run + __log2f(l_tot);
     bf16_t* op = out + ((size_t)row0 + min(qrow, L - 1)) * D + h * 64;
-    if (WIDE) {
-        // lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
+    {
+        // 16-B stores: lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
         // trades the lower lane's odd-g words for the upper lane's even-g words, so each lane
         // stores 8 consecutive d (16 B): the lower lane d = 16gp + 0..7, the upper 16gp + 8..15
 #pragma unroll
@@ -629,471 +465,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
                 if (qrow < L)
                     *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
             }
-    } else if (qrow < L) {
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int d0 = dt * 32 + 8 * g + 4 * h2;
-                uint2 w;
-                w.x = pack_bf2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-                w.y = pack_bf2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-                *reinterpret_cast<uint2*>(op + d0) = w;
-            }
-    }
-    if constexpr (TRACE) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stamp(4);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Persistent vision-tower variant (knob 893 = 381 | 512, selectable where 381 applies and no lse /
-// packed sequences are asked for; measured slower than 381): the 381 feature set (fixed-offset softmax, key 0 up front, one
-// barrier per key tile, asm V^T reads, 16-B stores, buffer-descriptor DMAs) on a grid of resident
-// workgroups walking the q-blocks in rounds.  The next block's Q rows, key-0 rows and
-// first K/V tile are LDS-DMA'd during the current block's last key tile, so a block starts on data
-// already in LDS: at L = 577 a q-block runs only 9 key tiles, and the start-up of a freshly
-// dispatched workgroup (Q and key 0 from HBM, tile 0's DMA, nothing to overlap with) had cost about
-// three tiles' worth per block (tools/bench_kernels.py: 788 TF/s at L = 577 against 1017 at L = 2305,
-// same FLOPs).  LDS: the K/V ring (2 x 16 KB), the Q image (128 rows x 128 B, 16-B chunk c of row r at
-// c ^ (r & 7): conflict-free ds_read_b128 of 8 rows), key 0's K and V rows (one DMA, 1 KB written).
-template <int VAR>
-__global__ __launch_bounds__(256, 3) void attn_fwd_p(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                     int L, int H, int nblk, float qscale,
-                                                     unsigned long long* __restrict__ trace = nullptr,
-                                                     int trace_n = 0) {
-    // PRIO (bit 8192): the workgroups resident on a CU keep their dispatch order for the whole launch,
-    // and VALU issue goes to the oldest wave of a SIMD first, so in the static rounds the youngest
-    // workgroup of every CU is the slowest all the way (per-block loop times +-15 %);
-    // each block sets s_setprio (blocks done + workgroup slot on the CU) mod 3, rotating the order
-    constexpr bool PRIO = (VAR & 8192) != 0;
-    // TRACE (bit 1024, diagnostics): per wave, the s_memrealtime time spent in block starts (the
-    // counted wait + barrier + Q / key-0 reads), in key-tile loops and in epilogues, the block count,
-    // and the wave's first and last stamps: trace[(block * 4 + wave) * 8 + 0..5]
-    constexpr bool TRACE = (VAR & 1024) != 0;
-    unsigned long long tr_wait = 0, tr_loop = 0, tr_epi = 0, tr_n = 0, tr_t = 0;
-    auto now = [&]() -> unsigned long long {
-        unsigned long long t = 0;
-        if constexpr (TRACE) {
-            t = __builtin_amdgcn_s_memrealtime();
-            asm volatile("" : "+s"(t));
-        }
-        return t;
-    };
-    constexpr int QOFF = 2 * STAGE_BYTES;
-    constexpr int COFF = QOFF + QBLK * 128;
-    __shared__ __attribute__((aligned(16))) char smem[COFF + 1024];
-    // blocks slot, slot + G, slot + 2G, ...: the grid walks the blocks in rounds, and slot is the XCD-aware
-    // remap of attn_fwd, so the q-blocks of one (batch, head) run at the same time on one XCD and
-    // share its K / V tiles in that XCD's L2 (contiguous runs per workgroup re-read every head's K / V
-    // from HBM once per q-block: 649 against 711 TF/s at L = 577, profiles/r05/r05j_*, r05k_*)
-    const int G = gridDim.x;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, qn = G >> 3, rn = G & 7;
-    const int blk_first = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
-    if (blk_first >= nblk) return;        // workgroup-uniform
-    const int nqb = (L + QBLK - 1) / QBLK;
-    const int D = H * 64;
-    const int ld2 = 6 * D;                // bytes per qkv row
-    const int Lk = L - 1;                 // keys 1 .. L - 1 fill the tiles (launcher: Lk % 64 == 0)
-    const int nkt = Lk / KBLK;
-    const int nrec = (Lk - 1) * ld2 + 128;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31;
-    const int h2 = lane >> 5;
-    // K/V staging (as attn_fwd): thread -> row tid >> 3 of a 32-row pass, 16-B chunk tid & 7
-    const int srow = tid >> 3;
-    const int spos = tid & 7;
-    const int kchunk = spos ^ ((tid >> 4) & 7);
-    const int vchunk = spos ^ (((srow >> 1) & 1) << 2);
-    int kvo[2], vvo[2];
-#pragma unroll
-    for (int ps = 0; ps < 2; ++ps) {
-        kvo[ps] = (ps * 32 + srow) * ld2 + kchunk * 16;
-        vvo[ps] = (ps * 32 + srow) * ld2 + vchunk * 16;
-    }
-    int koff[2][4];
-#pragma unroll
-    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const int row = kt2 * 32 + r;
-            koff[kt2][ks] = row * 128 + (((2 * ks + h2) ^ ((row >> 1) & 7)) << 4);
-        }
-    const int Gq = lane >> 4, gi = lane & 15;
-    const int vq = gi >> 2, vp = gi & 3;
-    unsigned vaddr[2];
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-        const int chunk = dt * 4 + 2 * (Gq & 1) + (vp >> 1);
-        const int voff = (4 * (Gq >> 1) + vq) * 128 + ((chunk ^ (((vq >> 1) & 1) << 2)) << 4) + (vp & 1) * 8;
-        vaddr[dt] = (unsigned)(uintptr_t)(CE_LDS void*)(smem + voff);
-    }
-    // Q image reads: row wave * 32 + r ((wave * 32 + r) & 7 = r & 7), 16-B chunk 2 ks + h2
-    int qoff[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qoff[ks] = QOFF + (wave * 32 + r) * 128 + (((2 * ks + h2) ^ (r & 7)) << 4);
-    // Q staging: wave w's 32 rows, 8 per DMA; lane -> row lane >> 3 of the 8, chunk (lane & 7) ^ (lane >> 3)
-    const int qchunk = (lane & 7) ^ (lane >> 3);
-
-    // block -> (batch, head, q-block); hb = byte address of row 0 of the sequence, column h * 64 (q third)
-    struct Blk {
-        int qb;
-        long orow0;                       // first output row of the sequence
-        int ocol;
-        const char* hb;
-    };
-    auto decode = [&](int bk) __attribute__((always_inline)) {
-        Blk k;
-        const int bh = bk / nqb;
-        k.qb = bk - bh * nqb;
-        const int b = bh / H, h = bh - b * H;
-        k.orow0 = (long)b * L;
-        k.ocol = h * 64;
-        k.hb = reinterpret_cast<const char*>(qkv) + (size_t)b * L * ld2 + h * 128;
-        return k;
-    };
-    auto stage_kv = [&](int t, auto bufc, __amdgpu_buffer_rsrc_t ks_, __amdgpu_buffer_rsrc_t vs_) __attribute__((always_inline)) {
-        constexpr int BUF = decltype(bufc)::value;
-        char* dst = smem + BUF * STAGE_BYTES + wave * 1024;
-        const int ro = t * KBLK * ld2;
-#pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-            // (the tile's row offset as the scalar offset: no per-tile VGPR offsets for hipcc to hoist)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ks_, (CE_LDS void*)(dst + ps * 4096), 16, kvo[ps], ro, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(vs_, (CE_LDS void*)(dst + TILE_KV_BYTES + ps * 4096), 16,
-                                                     vvo[ps], ro, 0, 0);
-        }
-    };
-    // Q rows (clamped to L - 1: the lanes past the end compute row L - 1's values again) and key 0's
-    // K / V rows (wave 0: lanes 0-7 K, 8-15 V, the rest repeat them into the area's unused bytes)
-    auto stage_q = [&](int qb, __amdgpu_buffer_rsrc_t qs_) __attribute__((always_inline)) {
-#pragma unroll
-        for (int ps = 0; ps < 4; ++ps) {
-            const int row = min(qb * QBLK + wave * 32 + ps * 8 + (lane >> 3), L - 1);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(qs_, (CE_LDS void*)(smem + QOFF + wave * 4096 + ps * 1024), 16,
-                                                     row * ld2 + qchunk * 16, 0, 0, 0);
-        }
-        if (wave == 0) {
-            const int i = lane & 15;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(qs_, (CE_LDS void*)(smem + COFF), 16,
-                                                     (i < 8 ? 2 * D : 4 * D) + (i & 7) * 16, 0, 0, 0);
-        }
-    };
-
-    Blk cur = decode(blk_first);
-    __amdgpu_buffer_rsrc_t qsrd = attn_srd(cur.hb, (L - 1) * ld2 + 128);
-    __amdgpu_buffer_rsrc_t ksrd = attn_srd(cur.hb + 2 * D + ld2, nrec);
-    __amdgpu_buffer_rsrc_t vsrd = attn_srd(cur.hb + 4 * D + ld2, nrec);
-    stage_q(cur.qb, qsrd);
-    stage_kv(0, std::integral_constant<int, 0>{}, ksrd, vsrd);
-    int par = 0;                          // ring slot of the block's tile 0
-    bool stores_out = false;              // the previous block's 4 output stores may be in flight
-    const f32x16 zero16 = {};
-
-    unsigned prio_n = 0;
-    unsigned long long tr_first = 0;
-    if constexpr (TRACE) tr_first = tr_t = now();
-    for (int blk = blk_first; blk < nblk; blk += G) {
-        if constexpr (PRIO) {
-            unsigned hw;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            const int pr = (int)((prio_n + ((hw >> 16) & 0xf)) % 3);
-            if (pr == 0) __builtin_amdgcn_s_setprio(0);
-            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(2);
-            ++prio_n;
-        }
-        // this block's Q, key-0 rows and K/V tile 0 landed (counted: the 4 stores after them may not)
-        if (stores_out) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier();
-        const int nblk_id = blk + G;
-        const bool has_next = nblk_id < nblk;
-        const Blk nxt = decode(has_next ? nblk_id : blk);
-        const __amdgpu_buffer_rsrc_t nqsrd = attn_srd(nxt.hb, (L - 1) * ld2 + 128);
-        const __amdgpu_buffer_rsrc_t nksrd = attn_srd(nxt.hb + 2 * D + ld2, nrec);
-        const __amdgpu_buffer_rsrc_t nvsrd = attn_srd(nxt.hb + 4 * D + ld2, nrec);
-        const int q_wave0 = cur.qb * QBLK + wave * 32;
-        const int qrow = q_wave0 + r;
-        const bool active = q_wave0 < L;  // wave-uniform
-
-        bf16x8 qf[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(smem + qoff[ks]);
-        if (qscale != 1.0f) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
-        }
-        // key 0: its score (v_dot2_f32_bf16 on the bf16 pairs, both lane halves summed) and its term in O / l
-        f32x16 o[2];
-        float m_run = 0.f, l_run = 0.f;
-        float s0v;
-        {
-            float a = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const bf16x8 kv = *reinterpret_cast<const bf16x8*>(smem + COFF + (2 * ks + h2) * 16);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const bf16x2_t qa = {qf[ks][2 * e], qf[ks][2 * e + 1]};
-                    const bf16x2_t ka = {kv[2 * e], kv[2 * e + 1]};
-                    a = __builtin_amdgcn_fdot2_f32_bf16(qa, ka, a, false);
-                }
-            }
-            s0v = a + __shfl_xor(a, 32, 64);
-        }
-        const bool fix_ok = __all(s0v <= 64.0f && s0v >= -64.0f);
-        bool fast = fix_ok;
-        float p0 = 1.0f;
-        if (fix_ok) p0 = __builtin_amdgcn_exp2f(s0v);
-        else m_run = s0v;
-        if (h2 == 0) l_run = p0;
-        // (key 0's V row by inline asm: the compiler would wait vmcnt(0) before a plain LDS read here, for
-        // the previous block's output stores)
-        uint2 v0w[2][4];
-        {
-            const unsigned va = (unsigned)(uintptr_t)(CE_LDS void*)(smem + COFF + 128 + 8 * h2);
-#define CE_V0(DT, G) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v0w[DT][G]) : "v"(va), "n"(((DT) * 32 + 8 * (G)) * 2))
-            CE_V0(0, 0); CE_V0(0, 1); CE_V0(0, 2); CE_V0(0, 3);
-            CE_V0(1, 0); CE_V0(1, 1); CE_V0(1, 2); CE_V0(1, 3);
-#undef CE_V0
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const uint2 w = v0w[dt][g];
-                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
-                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
-                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
-                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
-            }
-
-        auto pv_asm = [&](auto vbc, const bf16x8 (&pf)[2][2]) {
-            constexpr int VB = decltype(vbc)::value;
-            typedef __attribute__((ext_vector_type(8))) short s16x8;
-            s16x4 vr[2][2][2];
-#define CE_TRV(R, DT, H, OFF) \
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[R][DT][H]) : "v"(vaddr[DT]), "n"(OFF))
-#define CE_ISSUE(Q) \
-    CE_TRV((Q) & 1, 0, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
-    CE_TRV((Q) & 1, 0, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024); \
-    CE_TRV((Q) & 1, 1, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
-    CE_TRV((Q) & 1, 1, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024)
-            auto mf = [&](int q) __attribute__((always_inline)) {
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[q >> 1][q & 1],
-                                                                   o[dt], 0, 0, 0);
-                }
-            };
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (q == 0) { CE_ISSUE(0); }
-                else if (q == 1) { CE_ISSUE(1); }
-                else if (q == 2) { CE_ISSUE(2); }
-                else { CE_ISSUE(3); }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                mf(q);
-            }
-#undef CE_ISSUE
-#undef CE_TRV
-        };
-        auto rescale = [&](float delta) __attribute__((always_inline)) {
-            const float alpha = __builtin_amdgcn_exp2f(-delta);
-            l_run *= alpha;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-            m_run += delta;
-        };
-        auto tile = [&](const int t, auto bufc) __attribute__((always_inline)) {
-            constexpr int BUF = decltype(bufc)::value;
-            // tile t landed and every wave is done with tile t - 1 (tile 0: the block-start barrier; with a
-            // single tile, the Q / key-0 reads before the next block's DMAs overwrite them)
-            // the next block's Q / key-0 rows are staged at tile qt (tile 1 when there are >= 3 tiles:
-            // every wave has read this block's Q by tile 1's barrier), behind that tile's K / V DMAs, so
-            // tile qt + 1 waits for its own K / V only (counted: the Q pieces issued after them stay in
-            // flight) and they have two tiles to land; with fewer tiles, at the last tile
-            const int qt = nkt >= 3 ? 1 : nkt - 1;
-            if (t > 0 || nkt == 1) {
-                if (t == qt + 1 && has_next) {
-                    if (wave == 0) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-                    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                }
-                barrier();
-            }
-            if (t + 1 < nkt) {
-                stage_kv(t + 1, std::integral_constant<int, BUF ^ 1>{}, ksrd, vsrd);
-            } else if (has_next) {
-                stage_kv(0, std::integral_constant<int, BUF ^ 1>{}, nksrd, nvsrd);
-            }
-            if (t == qt && has_next) stage_q(nxt.qb, nqsrd);
-            const char* kb = smem + BUF * STAGE_BYTES;
-            bool redo = false;
-            const bool fast_tile = fast;   // wave-uniform
-            if (active && fast_tile) {
-                f32x16 s[2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) {
-                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
-                        s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? zero16 : s[kt2], 0, 0, 0);
-                    }
-                float ps[4] = {0.f, 0.f, 0.f, 0.f};
-                bf16x8 pf[2][2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
-                            ps[j & 3] += pv_;
-                            pf[kt2][s2][j] = (__bf16)pv_;
-                        }
-                const float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-                const bool overflow = __any(!(psum <= 0x1p64f)) || (t == 0 && __any(!(psum >= 0x1p-64f)));
-                if (!overflow) {
-                    l_run += psum;
-                    __builtin_amdgcn_sched_barrier(0);
-                    pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
-                } else {
-                    fast = false;
-                    redo = true;
-                }
-            }
-            if (active && (redo || !fast_tile)) {
-                // general online softmax (rare: a row max outside +-64 in log2 units)
-                f32x16 s[2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) s[kt2][i] = -m_run;
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) {
-                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
-                        s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
-                    }
-                }
-                float tmax = s[0][0];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax = fmaxf(tmax, s[kt2][i]);
-                tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-                const bool fix0 = t == 0 && fix_ok && __all(tmax <= 64.0f && tmax >= -64.0f);
-                if (fix0) fast = true;
-                if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
-                    const float delta = t == 0 ? fmaxf(tmax, s0v - m_run) : fmaxf(tmax, 0.f);
-                    rescale(delta);
-                    fast = false;
-#pragma unroll
-                    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) s[kt2][i] -= delta;
-                }
-                float psum = 0.f;
-                bf16x8 pf[2][2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
-                            psum += pv_;
-                            pf[kt2][s2][j] = (__bf16)pv_;
-                        }
-                l_run += psum;
-                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf);
-            }
-        };
-        auto run = [&](auto pc) __attribute__((always_inline)) {
-            constexpr int P = decltype(pc)::value;
-            for (int t = 0; t < nkt; t += 2) {
-                tile(t, std::integral_constant<int, P>{});
-                if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, P ^ 1>{});
-            }
-        };
-        unsigned long long tl0 = 0;
-        if constexpr (TRACE) {
-            tl0 = now();
-            tr_wait += tl0 - tr_t;
-        }
-        if (par) run(std::integral_constant<int, 1>{});
-        else run(std::integral_constant<int, 0>{});
-        if constexpr (TRACE) {
-            tr_t = now();
-            tr_loop += tr_t - tl0;
-        }
-
-        // epilogue: O = O^T / l, 16-B stores (lanes l, l^32 trade halves); rows past L repeat row L - 1
-        if (active) {
-            const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-            const float inv = 1.0f / l_tot;
-            bf16_t* op = out + (size_t)(cur.orow0 + min(qrow, L - 1)) * D + cur.ocol;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                for (int gp = 0; gp < 2; ++gp) {
-                    const int g0 = 2 * gp, g1 = 2 * gp + 1;
-                    const f32x2 iv = {inv, inv};
-                    const f32x2 a0 = f32x2{o[dt][4 * g0 + 0], o[dt][4 * g0 + 1]} * iv;
-                    const f32x2 a1 = f32x2{o[dt][4 * g0 + 2], o[dt][4 * g0 + 3]} * iv;
-                    const f32x2 b0 = f32x2{o[dt][4 * g1 + 0], o[dt][4 * g1 + 1]} * iv;
-                    const f32x2 b1 = f32x2{o[dt][4 * g1 + 2], o[dt][4 * g1 + 3]} * iv;
-                    const uint32_t ax = pack_bf2(a0.x, a0.y), ay = pack_bf2(a1.x, a1.y);
-                    const uint32_t bx = pack_bf2(b0.x, b0.y), by = pack_bf2(b1.x, b1.y);
-                    const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-                    const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-                    *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
-                }
-        }
-        stores_out = active;
-        if constexpr (TRACE) {
-            const unsigned long long te = now();
-            tr_epi += te - tr_t;
-            tr_t = te;
-            ++tr_n;
-        }
-        cur = nxt;
-        qsrd = nqsrd; ksrd = nksrd; vsrd = nvsrd;
-        par ^= nkt & 1;
-    }
-    if constexpr (TRACE) {
-        const long rec = (long)blockIdx.x * 4 + wave;
-        if (trace && rec < trace_n && lane == 0) {
-            unsigned hw, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            unsigned long long v[7] = {tr_wait, tr_loop, tr_epi, tr_n, tr_first, tr_t,
-                                       ((unsigned long long)xcc << 32) | hw};
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                asm volatile("" : "+v"(v[k]));
-                trace[rec * 8 + k] = v[k];
-            }
-        }
     }
 }
 
 std::atomic<int> g_attn_var{381};     // A/B knob (knobs.h: process-wide atomic)
-// diagnostics (ce_set_attn_trace): per-wave timeline of variant 1405 (= 381 with TRACE) launches
-std::atomic<unsigned long long*> g_attn_trace{nullptr};
-std::atomic<long> g_attn_trace_n{0};
 
 // One query row per (batch, head) against all of its sequence's keys (keys 0..pos with the causal
 // mask): the attention of a tower's last block when only the pooled row is consumed (CLS row b*L
@@ -1242,92 +617,21 @@ hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H,
 #define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
     const int v = g_attn_var.load(std::memory_order_acquire);
-    const bool clsk_ok = (L - 1) % KBLK == 0 && L > 1;
-    if (!causal && (v == 893 || v == 1917 || v == 9085 || v == 10109) && clsk_ok && !lse && !seg) {
-        // persistent: as many workgroups as fit on the device at once (occupancy per device, cached)
-        static std::atomic<int> occ[kMaxDevices];
-        const int dev = current_device();
-        int per_cu = occ[dev].load(std::memory_order_acquire);
-        if (per_cu <= 0) {
-            int q = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, reinterpret_cast<const void*>(attn_fwd_p<893>), 256, 0) !=
-                    hipSuccess || q <= 0)
-                q = 2;
-            const int ov = env_int("CE_ATTN_PERSIST_OCC", 0);      // A/B: workgroups per CU
-            if (env_int("CE_ATTN_DEBUG", 0)) fprintf(stderr, "attn_fwd_p: occupancy %d per CU, override %d\n", q, ov);
-            if (ov > 0) q = ov;
-            occ[dev].store(q, std::memory_order_release);
-            per_cu = q;
-        }
-        const long nblk = (long)((L + QBLK - 1) / QBLK) * H * B;
-        if (nblk > 0x7fffffffL) return hipErrorInvalidValue;
-        const int g = (int)std::min<long>(nblk, (long)per_cu * device_cus());
-        if (v == 1917)
-            hipLaunchKernelGGL((attn_fwd_p<1917>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
-                               g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
-        else if (v == 10109)
-            hipLaunchKernelGGL((attn_fwd_p<10109>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale,
-                               g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
-        else if (v == 9085)
-            hipLaunchKernelGGL((attn_fwd_p<9085>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
-        else
-            hipLaunchKernelGGL((attn_fwd_p<893>), dim3((unsigned)g), dim3(256), 0, s, qkv, out, L, H, (int)nblk, qscale);
-        return hipGetLastError();
-    }
     if (causal) {
-        if ((v & 88) == 88) CE_ATTN_LAUNCH(true, 88);
-        else if ((v & 24) == 24) CE_ATTN_LAUNCH(true, 24);
-        else if (v & 8) CE_ATTN_LAUNCH(true, 8);
-        else CE_ATTN_LAUNCH(true, 0);
+        CE_ATTN_LAUNCH(true, 88);
+    } else if (v == 381 && (L - 1) % KBLK == 0 && L > 1) {
+        // key 0 first (CLSK) needs the keys after the first to fill whole tiles
+        CE_ATTN_LAUNCH(false, 381);
     } else {
-        // CLSK needs the keys after the first to fill whole tiles
-        const int vv = (v == 893 || v == 1917 || v == 9085 || v == 10109) ? (clsk_ok ? 381 : 125)
-                     : (v == 1405 || v == 2429 || v == 3453) ? (clsk_ok ? v : 125)
-                     : (v & 256) && !clsk_ok ? (v & ~256) : v;
-        switch (vv) {
-            case 381: CE_ATTN_LAUNCH(false, 381); break;
-            case 2429: CE_ATTN_LAUNCH(false, 2429); break;
-            case 3453:
-                hipLaunchKernelGGL((attn_fwd<false, 3453>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg,
-                                   g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
-                break;
-            case 1405:
-                hipLaunchKernelGGL((attn_fwd<false, 1405>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg,
-                                   g_attn_trace.load(), (int)std::min<long>(g_attn_trace_n.load(), 1L << 30));
-                break;
-            case 125: CE_ATTN_LAUNCH(false, 125); break;
-            case 253: CE_ATTN_LAUNCH(false, 253); break;
-            case 61: CE_ATTN_LAUNCH(false, 61); break;
-            case 29: CE_ATTN_LAUNCH(false, 29); break;
-            case 16: CE_ATTN_LAUNCH(false, 16); break;
-            case 0: CE_ATTN_LAUNCH(false, 0); break;
-            case 2: CE_ATTN_LAUNCH(false, 2); break;
-            case 5: CE_ATTN_LAUNCH(false, 5); break;
-            case 9: CE_ATTN_LAUNCH(false, 9); break;
-            case 13: CE_ATTN_LAUNCH(false, 13); break;
-            case 1: CE_ATTN_LAUNCH(false, 1); break;
-            default:     // unreachable through set_attn_variant; keep the CLSK guard of vv anyway
-                if ((L - 1) % KBLK == 0 && L > 1) CE_ATTN_LAUNCH(false, 381);
-                else CE_ATTN_LAUNCH(false, 125);
-                break;
-        }
+        CE_ATTN_LAUNCH(false, 125);
     }
 #undef CE_ATTN_LAUNCH
     return hipGetLastError();
 }
 
-void set_attn_trace(unsigned long long* buf, long n) {
-    g_attn_trace_n.store(buf ? n : 0);
-    g_attn_trace.store(buf);
-}
-
 int set_attn_variant(int var) {
-    const int prev = g_attn_var.load();
-    g_attn_var = (var == 0 || var == 1 || var == 2 || var == 5 || var == 9 || var == 13 || var == 16 || var == 29 ||
-                  var == 61 || var == 125 || var == 253 || var == 381 || var == 893 || var == 1405 || var == 2429 ||
-                  var == 3453 || var == 1917 || var == 9085 || var == 10109)
-                     ? var : 381;
-    return prev;
+    // 381: key 0 ahead of the key tiles where (L - 1) % 64 == 0 (default); 125: the key tiles only
+    return g_attn_var.exchange(var == 125 ? 125 : 381);
 }
 
 }  // namespace ce

@@ -2180,11 +2180,6 @@ int ce_set_gemm_auto(int mode) { return ce::set_gemm_auto(mode); }
 int ce_set_gemm_variant(int bits) { return ce::set_gemm_variant(bits); }
 int ce_set_attn_variant(int var) { return ce::set_attn_variant(var); }
 int ce_set_fgemm_variant(int v) { return ce::set_fgemm_variant(v); }
-int ce_set_attn_trace(void* buf, int64_t n_waves) {
-    if (n_waves < 0) return fail(CE_ERR_INVALID, "ce_set_attn_trace: negative size");
-    ce::set_attn_trace((unsigned long long*)buf, (long)n_waves);
-    return CE_OK;
-}
 int ce_set_gemm_trace(void* buf, int64_t n_blocks) {
     if (n_blocks < 0) return fail(CE_ERR_INVALID, "ce_set_gemm_trace: negative size");
     ce::set_gemm_trace((unsigned long long*)buf, (long)n_blocks);

@@ -66,8 +66,9 @@ struct GemmParams {
     float* bwd_part = nullptr;
     // the process-wide schedule knobs (knobs.h), read once by launch_gemm so one launch never mixes
     // values another thread sets meanwhile
+    // (snap: set by the snapshot, so launch_gemm_act_bwd acts on gemm_act_bwd_fused's decision)
     struct {
-        int sched = 1, autom = 1, splitk = 1, groupm = 4, stagger = 0, ring = 4;
+        int sched = 1, autom = 1, splitk = 1, groupm = 4, stagger = 0, snap = 0;
     } kn;
 };
 // EPI_LN_STATS_HL: EPI_LN_STATS with the residual stream as hi/lo bf16 planes in and out;
@@ -77,18 +78,12 @@ hipError_t launch_gemm(const GemmParams& p, int act, bool out_bf16, hipStream_t 
 // dX GEMM of the MLP's c_proj in the text-tower backward with the activation backward and the c_fc
 // bias column sums in its epilogue (GemmParams::bwd_pre / bwd_part; act = the forward activation,
 // ACT_GELU or ACT_QGELU): the four-wave persistent kernel on the default policy, bf16 out, no bias /
-// residual, N % 128 == 0, out and bwd_pre of row stride N.  gemm_act_bwd_fused says whether a launch
-// would take it; launch_gemm_act_bwd returns hipErrorNotSupported otherwise (the caller then runs
-// launch_gemm + launch_act_bwd_colsum).  bwd_part holds (M + 127) / 128 rows of N floats.
-bool gemm_act_bwd_fused(const GemmParams& p, int act);
+// residual, N % 128 == 0, out and bwd_pre of row stride N.  gemm_act_bwd_fused takes the knob
+// snapshot into p and says whether a launch of that p takes the fused path; launch_gemm_act_bwd(p)
+// then decides on the same snapshot (hipErrorNotSupported if not fused: the caller runs launch_gemm +
+// launch_act_bwd_colsum).  bwd_part holds (M + 127) / 128 rows of N floats.
+bool gemm_act_bwd_fused(GemmParams& p, int act);
 hipError_t launch_gemm_act_bwd(const GemmParams& p, int act, hipStream_t s);
-// SCHED 13 (gemm_db.hip): bf16 output without residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0,
-// K >= 1024; `grid` persistent workgroups (p.gm set by the caller)
-hipError_t launch_gemm_db(const GemmParams& p, int act, int epi, int grid, hipStream_t s);
-// SCHED 14 (gemm_w2b.hip): two independent 256 x 128-tile workgroups per CU; bf16 output without
-// residual (EPI_PLAIN / EPI_LN_FOLD), N % 128 == 0, K % 32 == 0 (p.gm set by the caller)
-bool gemm_w2b_supported(const GemmParams& p, int epi, bool out_bf16, bool resid);
-hipError_t launch_gemm_w2b(const GemmParams& p, int act, int epi, hipStream_t s);
 // (mu, rstd) per row from the 64-column slab statistics of an EPI_LN_STATS launch (Chan's
 // combination; eps 1e-5): stats[r] from part[r][0 .. nslab-1]
 // (m_dev: packed rows, only the first *m_dev of the `rows` are live)
@@ -98,7 +93,7 @@ int set_gemm_schedule(int v);   // returns previous
 int current_gemm_sched();       // the current main-loop schedule (1 = default)
 int set_gemm_splitk(int on);     // split-K tail on/off (default on); returns previous
 int set_gemm_variant(int bits);  // kernel-variant bits for A/B (GEMM_VAR_*); returns previous
-int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 QKV-shape -> SCHED 11, ...); returns previous
+int set_gemm_auto(int mode);     // shape policy (CE_GEMM_AUTO: 0 off, 1 default, 2 / 3 wider SCHED 11); returns previous
 // launch counters per kernel path; index = path base + epilogue (EPI_PLAIN/LN_STATS/LN_FOLD)
 enum GemmPath { GEMM_PATH_W4PP = 0, GEMM_PATH_NT = 3, GEMM_PATH_FIXUP = 6, GEMM_PATH_OTHER = 9, GEMM_PATH_W2 = 10,
                 GEMM_PATH_COUNT = 13 };
@@ -129,8 +124,7 @@ int gemm_tn_split(int M, int N, int K, long part_elems);   // the K-split launch
 // q_prescaled: the q third of qkv already carries kAttnQScale (engine in_proj weights); else the
 // kernel scales its Q fragments.
 constexpr float kAttnQScale = 0.125f * 1.4426950408889634f;   // log2(e) / sqrt(64)
-int set_attn_variant(int var);
-void set_attn_trace(unsigned long long* buf, long n);   // diagnostics: per-wave timeline of variant 1405  // attention forward variant (0-2) for A/B; returns previous
+int set_attn_variant(int var);   // attention forward variant for A/B (381 default, 125; include/clipembed.h); returns previous
 int set_fgemm_variant(int v);   // 1 = register-blocked f32 GEMM (default), 0 = the 64 x 64 kernel
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse = nullptr,   // lse: [B][H][L] log2 log-sum-exp (training)

@@ -42,7 +42,6 @@ constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int NTHREADS = 512;
 constexpr int TILE_BYTES = BM * BK * 2;        // 32 KB per operand tile (BM == BN)
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // A + W
-constexpr int LOADS_PER_STAGE = 8;             // glds instructions per thread per stage
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ void barrier() {
@@ -65,14 +64,6 @@ __device__ __forceinline__ void wait_vm(int n) {
     else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
 }
 
-template <bool ON>
-__device__ __forceinline__ void wait_vm_if(int n) {
-    if constexpr (ON) wait_vm(n);
-}
-template <bool ON>
-__device__ __forceinline__ void barrier_if() {
-    if constexpr (ON) barrier();
-}
 
 // Epilogue: lane holds C[m = mbase + 16i + (lane&15)][n = nbase + 16j + 4(lane>>4) .. +3].
 // vmcnt counts stores as well as loads and retires in order, so a residual/bias load issued after
@@ -106,54 +97,32 @@ struct FoldOps {
     }
 };
 
-#ifndef CE_W4_EPI_HALVES
-#define CE_W4_EPI_HALVES 1
-#endif
-
 #ifndef CE_FOLD_PREFETCH
 #define CE_FOLD_PREFETCH 0
 #endif
 
-// kernel-variant bits (set_gemm_variant / env CE_GEMM_VARIANT), default GEMM_VAR_DEFAULT
-enum { GEMM_VAR_W4PP_NOWAIT = 1, GEMM_VAR_W4_EPI2 = 2,
-       // timing ablations of the four-wave LN-stats epilogue (wrong outputs; micro-benchmarks only)
-       GEMM_VAR_ABL_NORESID = 4, GEMM_VAR_ABL_NOSTORE = 8,
+// kernel-variant bits (set_gemm_variant / env CE_GEMM_VARIANT), default GEMM_VAR_DEFAULT.  Bit values
+// are kept from earlier rounds; the bits of the schedules measured and removed in round 6 (ablations,
+// DMA-split alternatives, SCHED 13 / 14 routing) are gone, and the two DMA-spread bits are always on.
+enum { GEMM_VAR_W4PP_NOWAIT = 1,
+       // the four-wave kernels' epilogues for one wave per SIMD (operands in an LDS side area); off: the
+       // residual-free and LN-statistics GEMMs stay on SCHED 1
+       GEMM_VAR_W4_EPI2 = 2,
        // the four-wave schedule with one tile per workgroup (grid = tiles): an exiting workgroup's
        // stores drain while the next one on the CU starts, instead of ahead of the next tile's DMAs
        GEMM_VAR_W4_ONETILE = 16,
        // split-K tail on the four-wave persistent schedule (a last round of <= 1/8 of the grid).
-       // Off by default; with EPI2 on a GELU GEMM its tail tiles finish in gemm_splitk_fixup with the
+       // Off by default; on a GELU GEMM its tail tiles finish in gemm_splitk_fixup with the
        // polynomial GELU (gelu_pair, <= 2.5e-6) while the main tiles use gelu_fast4 (<= 6.2e-5):
        // both far inside the bf16 output rounding, but A/B timings of this bit mix two epilogues
        GEMM_VAR_W4_TAIL = 32,
-       // timing ablation of the LN-statistics epilogues: no bf16 copy of the output (wrong xb)
-       GEMM_VAR_ABL_NOXB = 64,
        // the hi/lo residual GEMMs (EPI_LN_STATS_HL) on the staged-residual four-wave kernel
        GEMM_VAR_W4_RHL = 128,
-       // four-wave persistent schedule: a K-tile's 16 operand DMAs spread over B2 and B3 (one per
-       // ~6 MFMAs) instead of one per 4 MFMAs of B2 only
-       GEMM_VAR_W4_DMA_SPREAD = 256,
-       // the same spread on the staged-residual kernel's operand K-tiles
-       GEMM_VAR_RHL_DMA_SPREAD = 512,
-       // split of the spread four-wave schedule's 16 DMAs between B2 and B3: 12 + 4 or 8 + 8
-       // (default 10 + 6)
-       GEMM_VAR_W4_SPREAD12 = 1024, GEMM_VAR_W4_SPREAD8 = 2048,
-       // the 10 + 6 spread with B3's DMAs in the gaps that carry no fragment read
-       GEMM_VAR_W4_SPREAD_EVEN = 4096,
+       // (always on since round 6) a K-tile's 16 operand DMAs spread over B2 and B3
+       GEMM_VAR_W4_DMA_SPREAD = 256, GEMM_VAR_RHL_DMA_SPREAD = 512,
        // honour GemmParams::onetile: the caller's small grids (text tower) on the four-wave kernels
        // with one tile per workgroup instead of the 8-wave 4-phase kernel
-       GEMM_VAR_SMALL_ONETILE = 8192,
-       // (bits 14..18: SCHED 13 timing variants, gemm_db.hip)
-       // the staged-residual kernel drains every epilogue store before the next tile's K-loop
-       GEMM_VAR_RHL_DRAIN = 1 << 19,
-       // staged-residual kernel: rows 6-7's residual loaded in the last K-tile (ABL bit 4); staged-row
-       // reads kept as single ds_read_b64 (ABL bit 5)
-       GEMM_VAR_RHL_EARLY67 = 1 << 20, GEMM_VAR_RHL_NOREAD2 = 1 << 21,
-       // (bits 22-23: SCHED 14 timing variants, gemm_w2b.hip)
-       // the default schedule with the two-workgroup SCHED 14 kernel for: the hi/lo residual GEMMs of
-       // K <= 2048 (out-proj), every hi/lo residual GEMM, the LN-fold GEMMs (QKV / c_fc); big grids only
-       // (not the text tower's one-tile launches)
-       GEMM_VAR_W2B_OUT = 1 << 24, GEMM_VAR_W2B_RESID = 1 << 25, GEMM_VAR_W2B_FOLD = 1 << 26 };
+       GEMM_VAR_SMALL_ONETILE = 8192 };
 #ifndef CE_GEMM_VAR_DEFAULT
 #define CE_GEMM_VAR_DEFAULT \
     (GEMM_VAR_W4PP_NOWAIT | GEMM_VAR_W4_EPI2 | GEMM_VAR_W4_RHL | GEMM_VAR_W4_DMA_SPREAD | GEMM_VAR_RHL_DMA_SPREAD | \
@@ -322,7 +291,7 @@ __device__ __forceinline__ void gemm_epilogue_rows(const GemmParams& p, const f3
                         const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
                         const int mrow = (fq & 1) ? m : m - 16;
                         const size_t ob = (size_t)mrow * p.ldo + nbase + (fq & ~1) * 4 + j * 16;
-                        if ((!CHECK_M || mrow < p.M) && !(p.variant & GEMM_VAR_ABL_NOXB))
+                        if (!CHECK_M || mrow < p.M)
                             *reinterpret_cast<uint4*>(p.xb + ob) = make_uint4(x[0], y[0], x[1], y[1]);
                         if constexpr (HL_OUT) {
                             const auto xl = __builtin_amdgcn_permlane16_swap(plo[j].x, ol.x, false, false);
@@ -619,12 +588,10 @@ __device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 
     int xoff = ((fr + (fq & 1) * 16) * ldo + nbase + (fq >> 1) * 8) * 2;           // row pair, + j*32
     const int ostep = 16 * ldo * 4, rstep = 16 * ldr * 4, xstep = 32 * ldo * 2;
     f32x4 rv[RD][JN];
-    const bool abl_r = (p.variant & GEMM_VAR_ABL_NORESID) != 0, abl_s = (p.variant & GEMM_VAR_ABL_NOSTORE) != 0;
     auto load_r = [&](f32x4 (&r)[JN]) {     // the next fragment row's residual
 #pragma unroll
         for (int j = 0; j < JN; ++j)
-            r[j] = abl_r ? f32x4{0.f, 0.f, 0.f, 0.f}
-                         : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, roff + j * 64, 0, 0));
+            r[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, roff + j * 64, 0, 0));
         roff += rstep;
     };
 #pragma unroll
@@ -640,7 +607,7 @@ __device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 
             f32x4 v = acc[i][j];
             const f32x4 r = rv[i % RD][j];
             v[0] += bv[j].x + r[0]; v[1] += bv[j].y + r[1]; v[2] += bv[j].z + r[2]; v[3] += bv[j].w + r[3];
-            if (!abl_s) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), os, ooff + j * 64, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), os, ooff + j * 64, 0, 0);
             // Chan's pairwise update: the 4 values of block j join the lane's 4jj earlier ones
             const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
             const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
@@ -661,7 +628,7 @@ __device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 
                 const auto x = __builtin_amdgcn_permlane16_swap(pxb[j].x, o.x, false, false);
                 const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
                 const u32x4 d = {x[0], y[0], x[1], y[1]};
-                if (!abl_s) __builtin_amdgcn_raw_buffer_store_b128(d, xs, xoff + j * 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(d, xs, xoff + j * 32, 0, 0);
             }
         }
         ooff += ostep;
@@ -759,291 +726,11 @@ __device__ __forceinline__ void tile_of(int wgid, int tiles_m, int tiles_n, int 
     tm = first + (l - tn * gsz);
 }
 
-// ------------------------------------------------------------------------------------------
-// SCHED 6 ("early"): 2 whole-K-tile LDS buffers (BK = 64, 128 KB); all 8 LDS-DMA loads of
-// K-tile t+1 are issued at the start of K-tile t (its buffer was released by the previous
-// barrier), so they have a full K-tile of MFMA work (64 per wave) to land.  Inside a K-tile
-// there are no barriers: each wave walks its four 64x32 output quadrants (fragments read per
-// quadrant, 16 MFMAs each) and the two waves of a SIMD drift, overlapping one's LDS reads with
-// the other's MFMAs.  One vmcnt(0) + barrier per K-tile.  LDS image as SCHED 1 (128-B rows,
-// chunk c of row r at c ^ ((r>>1)&7)); staging by buffer_load ... lds descriptors.
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_early(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int nwg = ((p.M + BM - 1) / BM) * tiles_n;
-    const int wgid = xcd_remap(blockIdx.x, nwg);
-    int tm, tn;
-    tile_of(wgid, (p.M + BM - 1) / BM, tiles_n, p.gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    // staging: thread -> row (tid>>3) + 64*j (j = 0..3), 16-B chunk (tid&7); per wave-instruction
-    // 8 rows x 128 B = 1 KB lane-linear
-    const int srow = tid >> 3;
-    const int schunk = (tid & 7) ^ ((srow >> 1) & 7);
-    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
-    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
-    __amdgpu_buffer_rsrc_t srdA[4], srdW[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int ab = m0 + j * 64, wb = n0 + j * 64;
-        const int arows = max(0, min(p.M - ab, 64)), wrows = max(0, min(p.N - wb, 64));
-        srdA[j] = make_srd(p.A + (size_t)min(ab, p.M - 1) * p.lda, arows * (int)p.lda * 2);
-        srdW[j] = make_srd(p.W + (size_t)min(wb, p.N - 1) * p.ldw, wrows * (int)p.ldw * 2);
-    }
-    const int lds_wave = wave * 1024;
-    auto stage = [&](int kt, int buf) {
-        char* base = smem + buf * STAGE_BYTES + lds_wave;
-        const int kb = kt * BK * 2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA[j], (CE_LDS void*)(base + j * 8192), 16, voffA, kb, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW[j], (CE_LDS void*)(base + TILE_BYTES + j * 8192), 16, voffW,
-                                                     kb, 0, 0);
-    };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int frag_off0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
-    const int frag_off1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
-    const int a_off = wm * 128 * 128;
-    const int w_off = TILE_BYTES + wn * 64 * 128;
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    bf16x8 af[4][2], bfr[2][2];
-    auto readA = [&](const char* sb, int mh) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            af[i][0] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off0);
-            af[i][1] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off1);
-        }
-    };
-    auto readB = [&](const char* sb, int nh) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            bfr[j][0] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off0);
-            bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
-        }
-    };
-    auto mfma_q = [&](int mh, int nh) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
-    };
-
-    const int nk = p.K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        const char* sb = smem + cur * STAGE_BYTES;
-        if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-        readA(sb, 0);
-        readB(sb, 0);
-        mfma_q(0, 0);
-        readB(sb, 1);
-        mfma_q(0, 1);
-        readA(sb, 1);
-        mfma_q(1, 1);
-        readB(sb, 0);
-        mfma_q(1, 0);
-        if (kt + 1 < nk) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // K-tile t+1 landed; reads done
-            barrier();                                          // everyone's; buffer cur released
-        }
-    }
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// SCHED 9 ("persistent"): SCHED 1's 4-phase half-tile pipeline run as ONE continuous K-step
-// stream over all the tiles a workgroup owns.  Grid = one 512-thread workgroup per CU; the
-// workgroups of XCD x own a contiguous range of tile ids (stride 32 inside it).  During the last
-// K-step of tile i the half-tiles of tile i+1's first K-step are issued (same buffer parity
-// rules as inside a tile), so the next tile's loads land while tile i's epilogue runs, and the
-// epilogue's stores drain while tile i+1 computes.  Per tile the epilogue starts with
-// vmcnt(0) + barrier (tile i+1's step-0 half-tiles then are landed and visible), which lets the
-// first two waits of the next tile be skipped (they would otherwise wait for the stores).
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_persist(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int T = ((p.M + BM - 1) / BM) * tiles_n;
-    const int W8 = gridDim.x >> 3;                 // workgroups per XCD group (grid % 8 == 0)
-    const int xcd = blockIdx.x & 7;
-    const int q8 = T >> 3, r8 = T & 7;
-    const int xs = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-    const int xe = xs + q8 + (xcd < r8 ? 1 : 0);
-    const int first = xs + (blockIdx.x >> 3);
-    if (first >= xe) return;
-
-    // staging geometry (as SCHED 1 / 2): half-tile HA[h] = A rows h*64 + j*128 + rr, HB[h] = W rows
-    // (2j + (rr>>5))*64 + h*32 + (rr&31), j = 0..1, rr = tid>>3; chunk swizzle c ^ ((r>>1)&7)
-    const int rr = tid >> 3;
-    const int chunk = (tid & 7) ^ ((rr >> 1) & 7);
-    const int voffA = rr * (int)p.lda * 2 + chunk * 16;
-    const int voffB = ((rr >> 5) * 64 + (rr & 31)) * (int)p.ldw * 2 + chunk * 16;
-    int a_lds[2][2], w_lds[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            a_lds[h][j] = (h * 64 + j * 128 + wave * 8) * 128;
-            w_lds[h][j] = TILE_BYTES + ((j * 2 + ((wave * 8) >> 5)) * 64 + h * 32 + ((wave * 8) & 31)) * 128;
-        }
-    auto stageA = [&](int mt0, int kt, int buf, int h) {
-        char* base = smem + buf * STAGE_BYTES;
-        const int kb = kt * BK * 2;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int ab = mt0 + h * 64 + j * 128;
-            const int rows = max(0, min(p.M - ab, 64));
-            const __amdgpu_buffer_rsrc_t srd = make_srd(p.A + (size_t)min(ab, p.M - 1) * p.lda, rows * (int)p.lda * 2);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (CE_LDS void*)(base + a_lds[h][j]), 16, voffA, kb, 0, 0);
-        }
-    };
-    auto stageB = [&](int nt0, int kt, int buf, int h) {
-        char* base = smem + buf * STAGE_BYTES;
-        const int kb = kt * BK * 2;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int bb = nt0 + j * 128 + h * 32;
-            const int rows = max(0, min(p.N - bb, 96));
-            const __amdgpu_buffer_rsrc_t srd = make_srd(p.W + (size_t)min(bb, p.N - 1) * p.ldw, rows * (int)p.ldw * 2);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (CE_LDS void*)(base + w_lds[h][j]), 16, voffB, kb, 0, 0);
-        }
-    };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int frag_off0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
-    const int frag_off1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
-    const int a_off = wm * 128 * 128;
-    const int w_off = TILE_BYTES + wn * 64 * 128;
-    bf16x8 af[4][2], bfr[2][2];
-    f32x4 acc[8][4];
-    auto readA = [&](const char* sb, int mh) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            af[i][0] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off0);
-            af[i][1] = *reinterpret_cast<const bf16x8*>(sb + a_off + (mh * 4 + i) * 16 * 128 + frag_off1);
-        }
-    };
-    auto readB = [&](const char* sb, int nh) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            bfr[j][0] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off0);
-            bfr[j][1] = *reinterpret_cast<const bf16x8*>(sb + w_off + (nh * 2 + j) * 16 * 128 + frag_off1);
-        }
-    };
-    auto mfma_q = [&](int mh, int nh) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        bfr[j][ks], af[i][ks], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    };
-
-    const int nk = p.K / BK;
-    int tm = first / tiles_n;
-    int m0 = tm * BM, n0 = (first - tm * tiles_n) * BN;
-    // prologue: step 0 of the first tile, issue order A0, B0, B1, A1
-    stageA(m0, 0, 0, 0);
-    stageB(n0, 0, 0, 0);
-    stageB(n0, 0, 0, 1);
-    stageA(m0, 0, 0, 1);
-    wait_vm(4);
-    barrier();
-    int par = 0;                                   // buffer parity of the current K-step
-    for (int t = first; t < xe; t += W8) {
-        const bool has_next = t + W8 < xe;
-        int m0n = 0, n0n = 0;
-        if (has_next) {
-            const int tmn = (t + W8) / tiles_n;
-            m0n = tmn * BM;
-            n0n = (t + W8 - tmn * tiles_n) * BN;
-        }
-        const bool fresh = t != first;             // step-0 half-tiles already waited in the epilogue
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = par, nxt = par ^ 1;
-            const bool more = kt + 1 < nk;
-            const bool load = more || has_next;
-            const int lm = more ? m0 : m0n, ln = more ? n0 : n0n, lk = more ? kt + 1 : 0;
-            const bool skipw = fresh && kt == 0;
-            const char* sb = smem + cur * STAGE_BYTES;
-            // phase 1: quadrant (0,0); prefetch HA0(next step)
-            readA(sb, 0);
-            readB(sb, 0);
-            if (load) stageA(lm, lk, nxt, 0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(0, 0);
-            if (!skipw) wait_vm(load ? 4 : 0);     // HB1(this step)
-            barrier();
-            // phase 2: quadrant (0,1); prefetch HB0(next)
-            readB(sb, 1);
-            if (load) stageB(ln, lk, nxt, 0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(0, 1);
-            if (!skipw) wait_vm(load ? 4 : 0);     // HA1(this step)
-            barrier();
-            // phase 3: quadrant (1,1); prefetch HB1(next)
-            readA(sb, 1);
-            if (load) stageB(ln, lk, nxt, 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(1, 1);
-            barrier();
-            // phase 4: quadrant (1,0); prefetch HA1(next)
-            readB(sb, 0);
-            if (load) stageA(lm, lk, nxt, 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mfma_q(1, 0);
-            wait_vm(load ? 4 : 0);                 // HA0(next), HB0(next)
-            barrier();
-            par = nxt;
-        }
-        // next tile's step-0 half-tiles all landed and visible before the epilogue's traffic
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier();
-        gemm_epilogue<ACT, HAS_RESID, OUT_BF16>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
-        m0 = m0n;
-        n0 = n0n;
-    }
-}
-
-// SCHED 0: 2-stage ring, whole-tile stages, 2 barriers per K-tile (reference schedule).
 // SCHED 1: 4 phases per K-tile; the K-tile is split in half-tiles {A rows of quadrant-row mh,
 //          W rows of quadrant-col nh}, each double-buffered; phase p computes one 64x32
 //          quadrant of every wave's 128x64 output (16 MFMAs) and issues the LDS-DMA of one
 //          half-tile of K-tile t+1, so every load has ~3 phases to land; one barrier per phase.
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int SCHED, int RING = CE_RESID_RING, int EPI = EPI_PLAIN>
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int RING = CE_RESID_RING, int EPI = EPI_PLAIN>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
     trace_stamp(p, 0);
@@ -1061,11 +748,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
     const int nwg = tiles_m * tiles_n;
     int bid = blockIdx.x;
     const int nk = p.K / BK;
-    // split-K tail (SCHED 1): blocks past t_main (dispatched last, so they fill the final, otherwise
+    // split-K tail: blocks past t_main (dispatched last, so they fill the final, otherwise
     // mostly idle round of the grid) each take one K-chunk of one of the last `tail` tiles
-    const int t_main = nwg - (SCHED == 1 ? p.tail : 0);
+    const int t_main = nwg - p.tail;
     int wgid, kt0 = 0, kt1 = nk, slab = -1;
-    if (SCHED == 1 && p.tail_only) bid += t_main;      // only the split-K chunks (SCHED 11's tail)
+    if (p.tail_only) bid += t_main;      // only the split-K chunks (SCHED 11's tail)
     if (bid < t_main) {
         // (packed rows: the live tiles are the first tile indices; blockIdx order spreads them over
         // the XCDs round-robin instead of the first XCDs' contiguous ranges)
@@ -1103,64 +790,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (SCHED == 0) {
-        // ---- staging addresses: thread -> (row tid>>3 of a 64-row pass, 16-B chunk) -----
-        const int srow = tid >> 3;
-        const int schunk = (tid & 7) ^ ((tid >> 4) & 7);   // inverse of the LDS swizzle
-        const bf16_t* a_src[4];
-        const bf16_t* w_src[4];
-#pragma unroll
-        for (int ps = 0; ps < 4; ++ps) {
-            int ar = min(m0 + ps * 64 + srow, p.M - 1);
-            int wr = min(n0 + ps * 64 + srow, p.N - 1);
-            a_src[ps] = p.A + (size_t)ar * p.lda + schunk * 8;
-            w_src[ps] = p.W + (size_t)wr * p.ldw + schunk * 8;
-        }
-        const int lds_wave_off = wave * 1024;
-        auto stage = [&](int kt, int buf) {
-            char* base = smem + buf * STAGE_BYTES + lds_wave_off;
-            const int koff = kt * BK;
-#pragma unroll
-            for (int ps = 0; ps < 4; ++ps) glds16(a_src[ps] + koff, base + ps * 8192);
-#pragma unroll
-            for (int ps = 0; ps < 4; ++ps) glds16(w_src[ps] + koff, base + TILE_BYTES + ps * 8192);
-        };
-        const int a_off = wm * 128 * 128;
-        const int w_off = TILE_BYTES + wn * 64 * 128;
-        stage(0, 0);
-        if (nk > 1) stage(1, 1);
-        for (int kt = 0; kt < nk; ++kt) {
-            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            barrier();
-            const char* sb = smem + (kt & 1) * STAGE_BYTES;
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const int fo = ks ? frag_off1 : frag_off0;
-                bf16x8 af[8], wf[4];
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    af[i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 128 + fo);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    wf[j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 128 + fo);
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
-            }
-            // every wave's fragment reads of this buffer must have landed before it is restaged
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            barrier();
-            if (kt + 2 < nk) stage(kt + 2, kt & 1);
-        }
-    } else if constexpr (SCHED == 1 || SCHED == 3 || SCHED == 4 || SCHED == 7) {
-        // SCHED 3/4/7: timing ablations of SCHED 1 (3: no global loads; 4: no loads, no barriers;
-        // 7: loads issued but never waited for).  Wrong results; micro-benchmark only.
-        constexpr bool LOADS = SCHED == 1 || SCHED == 7;
-        constexpr bool WAITS = SCHED == 1;
-        constexpr bool BARS = SCHED != 4;
+    {
         // ---- half-tile staging ---------------------------------------------------------------
         // LDS per buffer: A image rows 0..255 (32 KB) then W image rows 0..255 (32 KB), 128-B rows,
         // chunk c of row r at c ^ ((r>>1)&7).  Half-tile HA[mh] = A rows {mh*64 + j*128 + 0..63},
@@ -1186,14 +816,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
                 w_lds[h][j] = TILE_BYTES + wrow_w * 128;
             }
         auto stageA = [&](int kt, int buf, int h) {
-            if constexpr (!LOADS) return;
             char* base = smem + buf * STAGE_BYTES;
             const int koff = kt * BK;
             glds16(a_src[h][0] + koff, base + a_lds[h][0]);
             glds16(a_src[h][1] + koff, base + a_lds[h][1]);
         };
         auto stageB = [&](int kt, int buf, int h) {
-            if constexpr (!LOADS) return;
             char* base = smem + buf * STAGE_BYTES;
             const int koff = kt * BK;
             glds16(w_src[h][0] + koff, base + w_lds[h][0]);
@@ -1207,8 +835,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
         stageB(kt0, 0, 0);
         stageB(kt0, 0, 1);
         stageA(kt0, 0, 1);
-        if (kt1 - kt0 > 1) wait_vm_if<WAITS>(4); else wait_vm_if<WAITS>(0);
-        barrier_if<BARS>();
+        if (kt1 - kt0 > 1) wait_vm(4); else wait_vm(0);
+        barrier();
 
         bf16x8 af[4][2], bfr[2][2];
         auto readA = [&](const char* sb, int mh) {
@@ -1251,26 +879,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_nt(GemmParams p) {
             readA(sb, 0);
             readB(sb, 0);
             phase(0, 0, [&] { if (more) stageA(kt + 1, nxt, 0); });
-            wait_vm_if<WAITS>(more ? 4 : 0);        // HB1(t) landed
-            barrier_if<BARS>();
+            wait_vm(more ? 4 : 0);        // HB1(t) landed
+            barrier();
             // phase 2: quadrant (0,1); prefetch HB0(t+1)
             readB(sb, 1);
             phase(0, 1, [&] { if (more) stageB(kt + 1, nxt, 0); });
-            wait_vm_if<WAITS>(more ? 4 : 0);        // HA1(t) landed
-            barrier_if<BARS>();
+            wait_vm(more ? 4 : 0);        // HA1(t) landed
+            barrier();
             // phase 3: quadrant (1,1); prefetch HB1(t+1)
             readA(sb, 1);
             phase(1, 1, [&] { if (more) stageB(kt + 1, nxt, 1); });
-            barrier_if<BARS>();
+            barrier();
             // phase 4: quadrant (1,0); prefetch HA1(t+1)
             readB(sb, 0);
             phase(1, 0, [&] { if (more) stageA(kt + 1, nxt, 1); });
-            wait_vm_if<WAITS>(more ? 4 : 0);        // HA0(t+1), HB0(t+1) landed
-            barrier_if<BARS>();
+            wait_vm(more ? 4 : 0);        // HA0(t+1), HB0(t+1) landed
+            barrier();
         }
     }
 
-    if (SCHED == 1 && slab >= 0) {
+    if (slab >= 0) {
         // split-K tail chunk: raw f32 partial tile, row-major [256][256], slab `slab` of p.part
         float* dst = p.part + (size_t)slab * (BM * BN) + (size_t)(wm * 128 + fr) * BN + wn * 64 + fq * 4;
 #pragma unroll
@@ -1365,279 +993,27 @@ __global__ __launch_bounds__(256) void gemm_splitk_fixup(GemmParams p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// SCHED 2 ("w4"): the 256x256 tile computed by FOUR waves (one per SIMD), each owning a 128x128
-// quadrant: acc[8][8] = 256 f32 per lane pinned in AGPRs, so a fragment read feeds 8 MFMAs (LDS
-// reads per MFMA 0.25 vs 0.44 for SCHED 1).  One wave per SIMD has no partner to hide latency, so
-// the pipeline is explicit: BK = 32 steps through a 4-slot LDS ring (32 KB per slot: A and W
-// 256 rows x 64 B, chunk c of row r at c ^ 2((r>>2)&1): conflict-free for the four 16-lane groups
-// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... in which gfx950 serves ds_read_b128), DMA issued
-// four steps ahead (slots 0..3 in flight from the prologue), fragments of step s+1 read while
-// the 64 MFMAs of step s run:
-//    [frags(s) in regs] wait DMA(s+1) | barrier | DMA(s+4) -> slot s%4 | read frags(s+1) | MFMA(s)
-// One barrier per step.
-constexpr int W4_BK = 32;
-constexpr int W4_SLOT = 2 * BM * W4_BK * 2;     // 32 KB: A then W
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__global__ __launch_bounds__(256, 1) void gemm_bf16_w4(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[4 * W4_SLOT];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int tiles_m = (p.M + BM - 1) / BM;
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int nwg = tiles_m * tiles_n;
-    const int wgid = xcd_remap(blockIdx.x, nwg);
-    int tm, tn;
-    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    // staging: wave-instruction j moves rows j*64 + wave*16 + (lane>>2), 64-B row segments
-    const int srow = wave * 16 + (lane >> 2);
-    const int schunk = (lane & 3) ^ (((srow >> 2) & 1) << 1);  // row bit 2 of j*64 + srow == of srow
-    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
-    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
-    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
-    const __amdgpu_buffer_rsrc_t srdW = make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, BN)) * (int)p.ldw * 2);
-    const int lds_wave = wave * 1024;
-    const int ns = p.K / W4_BK;      // even, >= 2 (K % 64 == 0)
-    // steps past K are still issued (the loop stays branch-free and vmcnt counts stay constant)
-    // but with an offset beyond the descriptor's range: no memory traffic, LDS slot never read
-    auto stage = [&](int ks) {
-        char* base = smem + (ks & 3) * W4_SLOT + lds_wave;
-        const int kb = ks < ns ? ks * W4_BK * 2 : 0x7ffff000;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + j * 4096), 16,
-                                                     voffA + j * 64 * (int)p.lda * 2, kb, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + W4_SLOT / 2 + j * 4096), 16,
-                                                     voffW + j * 64 * (int)p.ldw * 2, kb, 0, 0);
-    };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int frag_off = fr * 64 + ((fq ^ (((fr >> 2) & 1) << 1)) << 4);
-    const int a_off = wm * 128 * 64 + frag_off;
-    const int w_off = W4_SLOT / 2 + wn * 128 * 64 + frag_off;
-
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    bf16x8 af[2][8], bf[2][8];   // [register set][block]
-    auto read_b = [&](int ks, int r) {
-        const char* sb = smem + (ks & 3) * W4_SLOT;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bf[r][j] = *reinterpret_cast<const bf16x8*>(sb + w_off + j * 16 * 64);
-    };
-    auto read_a = [&](int ks, int r) {
-        const char* sb = smem + (ks & 3) * W4_SLOT;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) af[r][i] = *reinterpret_cast<const bf16x8*>(sb + a_off + i * 16 * 64);
-    };
-    auto read_frags = [&](int ks, int r) { read_b(ks, r); read_a(ks, r); };
-    // inline-asm MFMA with the accumulator pinned in place in AGPRs ("+a"): with the builtin,
-    // hipcc shuffles part of the 256 accumulators between AGPRs and VGPRs every step
-    auto mfma_rows = [&](int r, int i0, int i1) {
-#pragma unroll
-        for (int i = i0; i < i1; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                             : "+a"(acc[i][j]) : "v"(bf[r][j]), "v"(af[r][i]));
-    };
-
-    stage(0);
-    stage(1);
-    stage(2);
-    stage(3);
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    barrier();
-    read_frags(0, 0);
-    // one step: DMA(st+1) landed (st+2, st+3 in flight) -> barrier -> DMA(st+4) into st's slot ->
-    // next fragments in two batches of 8 under this step's MFMAs (lgkmcnt encodes <= 15)
-    auto step = [&](int st, int u) {
-        // DMA(st+1) landed; this wave's reads of slot st (frags(st), issued last step) are done,
-        // so after the barrier nobody reads slot st and DMA(st+4) may overwrite it
-        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-        barrier();
-        stage(st + 4);
-        read_b(st + 1, u ^ 1);
-        mfma_rows(u, 0, 4);
-        read_a(st + 1, u ^ 1);
-        mfma_rows(u, 4, 8);
-    };
-    for (int s0 = 0; s0 < ns - 2; s0 += 2) {   // uniform body: the register set is a constant
-        step(s0, 0);
-        step(s0 + 1, 1);
-    }
-    step(ns - 2, 0);
-    mfma_rows(1, 0, 8);
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// SCHED 10 ("w4p"): 4 waves (one per SIMD), 128x128 per wave (acc[8][8] in AGPRs), BK = 64 with
-// two 64-KB LDS buffers and global prefetch two K-tiles deep.  All fragments of a K-tile live in
-// registers (two sets: k 0-31 and k 32-63), so a buffer is free as soon as the reads of its second
-// set have landed, long before the MFMAs finish with it; the DMA of K-tile t+2 then goes into the
-// buffer of K-tile t.  Per K-tile, 128 MFMAs in three interleaved blocks:
-//   B1: MFMA(set0, rows 0-3)  + 16 ds_read (set1 of t)          -> lgkmcnt(0), barrier
-//   B2: MFMA(set0, rows 4-7) + MFMA(set1, rows 0-3) + 16 DMA (t+2 -> this buffer)
-//                                                              -> vmcnt(16) (t+1 landed), barrier
-//   B3: MFMA(set1, rows 4-7)  + 16 ds_read (set0 of t+1, other buffer)
-// Interleaving by sched_group_barrier (MFMA/DS/VMEM classes); 2 barriers per K-tile.  LDS image as
-// SCHED 1 (128-B rows, chunk c of row r at c ^ ((r>>1)&7)).  Past-K DMAs are issued with an
-// out-of-range offset (no traffic) so every iteration is identical.
-template <int ACT, bool HAS_RESID, bool OUT_BF16>
-__global__ __launch_bounds__(256, 1) void gemm_bf16_w4p(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int tiles_m = (p.M + BM - 1) / BM;
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int nwg = tiles_m * tiles_n;
-    const int wgid = xcd_remap(blockIdx.x, nwg);
-    int tm, tn;
-    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int nk = p.K / BK;
-
-    // staging: instruction j of wave w moves rows j*32 + w*8 + (lane>>3), 16-B chunk lane&7 of the
-    // LDS row, fetched from source chunk (lane&7) ^ ((row>>1)&7)
-    const int srow = wave * 8 + (lane >> 3);
-    const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
-    const int voffA = srow * (int)p.lda * 2 + schunk * 16;
-    const int voffW = srow * (int)p.ldw * 2 + schunk * 16;
-    const int jstrA = 32 * (int)p.lda * 2, jstrW = 32 * (int)p.ldw * 2;
-    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
-    const __amdgpu_buffer_rsrc_t srdW = make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, BN)) * (int)p.ldw * 2);
-    auto dma = [&](int kt, int buf, int j) {     // j 0..7: A, 8..15: W
-        const int kb = kt < nk ? kt * BK * 2 : 0x7ffff000;
-        char* base = smem + buf * STAGE_BYTES;
-        if (j < 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + (j * 32 + wave * 8) * 128), 16,
-                                                     voffA + j * jstrA, kb, 0, 0);
-        else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + TILE_BYTES + ((j - 8) * 32 + wave * 8) * 128),
-                                                     16, voffW + (j - 8) * jstrW, kb, 0, 0);
-    };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int fo0 = fr * 128 + (((0 + fq) ^ (fr >> 1)) << 4);
-    const int fo1 = fr * 128 + (((4 + fq) ^ (fr >> 1)) << 4);
-    const int a_off = wm * 128 * 128;
-    const int w_off = TILE_BYTES + wn * 128 * 128;
-
-    f32x4 acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 a0[8], b0[8], a1[8], b1[8];
-
-    // prologue: K-tiles 0 and 1 in flight, set0 of K-tile 0
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dma(0, 0, j);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dma(1, 1, j);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    barrier();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        a0[q] = *reinterpret_cast<const bf16x8*>(smem + a_off + q * 16 * 128 + fo0);
-        b0[q] = *reinterpret_cast<const bf16x8*>(smem + w_off + q * 16 * 128 + fo0);
-    }
-
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        const char* sb = smem + buf * STAGE_BYTES;
-        const char* so = smem + (buf ^ 1) * STAGE_BYTES;
-        // ---- B1 ----
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            b1[q] = *reinterpret_cast<const bf16x8*>(sb + w_off + q * 16 * 128 + fo1);
-            a1[q] = *reinterpret_cast<const bf16x8*>(sb + a_off + q * 16 * 128 + fo1);
-        }
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- B2 ----
-#pragma unroll
-        for (int i = 4; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) dma(kt + 2, buf, j);
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- B3 ----
-#pragma unroll
-        for (int i = 4; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            a0[q] = *reinterpret_cast<const bf16x8*>(so + a_off + q * 16 * 128 + fo0);
-            b0[q] = *reinterpret_cast<const bf16x8*>(so + w_off + q * 16 * 128 + fo0);
-        }
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 2);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
-}
-
-// ------------------------------------------------------------------------------------------
-// SCHED 11 ("w4p persistent"): SCHED 10's main loop as one continuous K-tile stream over the
-// tiles a workgroup owns (grid = one workgroup per CU; tile r*grid + xcd_remap(b) in round r).
-// The DMA two K-tiles ahead runs into the next tile's first K-tiles, so the next tile's
-// operands are in flight while this tile's epilogue runs and there is no per-tile prologue.
-// EV bit 0: epilogue for one wave per SIMD with the side area (GEMM_VAR_W4_EPI2); bit 1: DMA
-// spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD)
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN, int EV = 0>
+// SCHED 11 (four-wave persistent): 4 waves (one per SIMD), 128x128 per wave (acc[8][8] pinned in
+// AGPRs), BK = 64, two 64-KB stage buffers (LDS image as SCHED 1: 128-B rows, chunk c of row r at
+// c ^ ((r>>1)&7)), run as one continuous K-tile stream over the tiles a workgroup owns (grid = one
+// workgroup per CU; tile r*grid + xcd_remap(b) in round r).  The DMA two K-tiles ahead runs into
+// the next tile's first K-tiles, so the next tile's operands are in flight while this tile's
+// epilogue runs and there is no per-tile prologue.  Epilogue for one wave per SIMD with its
+// operands in an LDS side area (w4_epilogue_bf16 / _stats / _act_bwd); a K-tile's 16 operand DMAs
+// spread over B2 (10, one per 6 MFMAs) and B3 (6).  (Measured and removed in round 6: whole-tile
+// and BK = 32 rings, non-persistent and early-DMA schedules, the 12+4 / 8+8 / even-gap DMA splits,
+// the register epilogue)
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
-    constexpr bool SIDE = (EV & 1) != 0;
-    constexpr bool SPREAD = (EV & 2) != 0;
+    // the epilogues of w4_ok (host side): bf16 without residual, the f32 LN-statistics residual, plain f32
+    constexpr bool EPI_F32 = !OUT_BF16 && !HAS_RESID && EPI == EPI_PLAIN && ACT == ACT_NONE;
+    static_assert((OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) || (EPI == EPI_LN_STATS && HAS_RESID && !OUT_BF16) ||
+                  EPI_F32, "four-wave epilogues: bf16 without residual, the f32 LN-statistics residual, plain f32");
     // DMAs of a K-tile issued in B2 (the rest in B3); the B2 wait leaves exactly these in flight
-    constexpr int DMA_B2 = !SPREAD ? 16 : (EV & 4) ? 12 : (EV & 8) ? 8 : 10;
+    constexpr int DMA_B2 = 10;
     constexpr int P2 = 64 / DMA_B2;                          // MFMAs per DMA in B2
-    constexpr int P3 = DMA_B2 < 16 ? 32 / (16 - DMA_B2) : 32; // and in B3
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + (SIDE ? 4 * W4_SIDE_BYTES : 0)];
+    constexpr int P3 = 32 / (16 - DMA_B2);                   // and in B3
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1748,12 +1124,11 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     // the fragments each MFMA reads.
 #define CE_MFMA_AGPR(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
-    // first K-tile of a tile (EV 1): C = 0 instead of zeroing 256 accumulators per tile
+    // (C = 0 form of the MFMA: a first K-tile that skips zeroing the accumulators; unused)
 #define CE_MFMA_AGPR0(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(BV), "v"(AV))
-    constexpr bool NEWLOOP = SIDE;
     // K-tile phases.  ZERO: first K-tile of a tile (C = 0 on each accumulator's first MFMA).
-    // B3's PRE: read set0 of the next K-tile under its MFMAs; with EV 1 the last K-tile of a tile
+    // B3's PRE: read set0 of the next K-tile under its MFMAs; the last K-tile of a tile
     // does not (the next tile's set0 is read after the epilogue, so the epilogue has those 64
     // VGPRs), reading it after the epilogue instead (read_set0).
     auto B1 = [&](const char* sb, auto zero) __attribute__((always_inline)) {
@@ -1779,11 +1154,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             } else {
                 CE_MFMA_AGPR(acc[i][j], b1[j], a1[i]);
             }
-            if constexpr (SPREAD) {
-                if (s2 % P2 == P2 - 1 && s2 / P2 < DMA_B2) dma(buf, s2 / P2, live);
-            } else {
-                if ((s2 & 3) == 3) dma(buf, s2 >> 2, live);
-            }
+            if (s2 % P2 == P2 - 1 && s2 / P2 < DMA_B2) dma(buf, s2 / P2, live);
         }
     };
     auto B3 = [&](const char* so, auto pre, int buf, bool live) __attribute__((always_inline)) {
@@ -1791,15 +1162,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         for (int s2 = 0; s2 < 32; ++s2) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
-            if constexpr (SPREAD) {
-                if constexpr ((EV & 16) != 0 && DMA_B2 == 10) {
-                    // placed in even gaps only (the odd ones carry a set-0 fragment read)
-                    if (s2 == 4 || s2 == 10 || s2 == 14 || s2 == 20 || s2 == 24 || s2 == 30)
-                        dma(buf, DMA_B2 + (s2 - 4) / 5, live);
-                } else if (s2 % P3 == P3 - 1 && DMA_B2 + s2 / P3 < 16) {
-                    dma(buf, DMA_B2 + s2 / P3, live);
-                }
-            }
+            if (s2 % P3 == P3 - 1 && DMA_B2 + s2 / P3 < 16) dma(buf, DMA_B2 + s2 / P3, live);
             if constexpr (decltype(pre)::value) {
                 if (s2 & 1) {
                     const int q = s2 >> 1;      // a0[0], b0[0..7], a0[1..7]
@@ -1827,7 +1190,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
         // one K-tile: B1 | barrier | B2 + DMA(step g+2) | wait + barrier | B3
         auto ktile = [&](int kt, auto pre) __attribute__((always_inline)) {
             // epilogue operands of this tile into the side area; retired by this K-tile's B2 wait
-            if (SIDE && kt == nk - 1) w4_side_fill<EPI>(p, side, tm * BM + wm * 128, tn * BN + wn * 128, lane);
+            if (kt == nk - 1) w4_side_fill<EPI>(p, side, tm * BM + wm * 128, tn * BN + wn * 128, lane);
             const int buf = g & 1;
             const char* sb = smem + buf * STAGE_BYTES;
             const char* so = smem + (buf ^ 1) * STAGE_BYTES;
@@ -1835,56 +1198,45 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             B1(sb, F_{});
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             barrier();
-            // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); DMA of step g+2 (one per 4) ----
+            // ---- B2: MFMA(set0, rows 4-7), MFMA(set1, rows 0-3); 10 DMAs of step g+2 (one per 6) ----
             const bool live = g + 2 < nsteps;
             B2(buf, live, F_{});
-            if constexpr (!SPREAD) advance();
             // K-tile g+1 landed.  Right after an epilogue (kt == 0 of a later tile) it already has:
             // the epilogue began with vmcnt(0) and B1 ended with a barrier.  Waiting here would also
             // drain every store of that epilogue (vmcnt retires loads, DMAs and stores in issue
             // order), exposing their write latency; skipped, they drain under this tile's MFMAs.
             if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA_B2) : "memory");
             barrier();
-            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it (and, SPREAD,
-            // the rest of step g+2's DMAs: buf's last reader was B1, before the first barrier) ----
+            // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it, and the rest of
+            // step g+2's DMAs (buf's last reader was B1, before the first barrier) ----
             B3(so, pre, buf, live);
-            if constexpr (SPREAD) advance();
+            advance();
             ++g;
         };
-        if constexpr (NEWLOOP) {
-            // the last K-tile does not read the next tile's set0 (read after the epilogue, which
-            // then has those 64 VGPRs)
-            for (int kt = 0; kt < nk - 1; ++kt) ktile(kt, T_{});
-            ktile(nk - 1, F_{});
-        } else {
-            for (int kt = 0; kt < nk; ++kt) ktile(kt, T_{});
-        }
+        // the last K-tile does not read the next tile's set0 (read after the epilogue, which then
+        // has those 64 VGPRs)
+        for (int kt = 0; kt < nk - 1; ++kt) ktile(kt, T_{});
+        ktile(nk - 1, F_{});
         trace_stamp(p, 1, t * grid + blockIdx.x);
         // the next tile's K-tile 1 (DMA issued in this tile's last B2) retires before any epilogue
         // load or store is issued (see the B2 wait above)
         if (nowait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (SIDE && OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) {
-            w4_epilogue_bf16<ACT, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
-        } else if constexpr (SIDE && EPI == EPI_LN_STATS) {
+        if constexpr (EPI == EPI_LN_STATS) {
             w4_epilogue_stats(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
+        } else if constexpr (OUT_BF16) {
+            w4_epilogue_bf16<ACT, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128, lane, side);
         } else {
-#if CE_W4_EPI_HALVES
-        // the 128-column quadrant as two 64-column epilogues: the NJ = 4 path (4-deep residual
-        // ring, a quarter of the live epilogue registers)
+            // plain f32 output: the register epilogue as two 64-column halves (NJ = 4 path)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            f32x4 q[8][4];
+            for (int h = 0; h < 2; ++h) {
+                f32x4 q[8][4];
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+                for (int i = 0; i < 8; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) q[i][j] = acc[i][h * 4 + j];
-            gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>(
-                p, q, tm * BM + wm * 128, tn * BN + wn * 128 + h * 64, lane);
-        }
-#else
-        gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 8, CE_RESID_RING, EPI>(p, acc, tm * BM + wm * 128, tn * BN + wn * 128,
-                                                                     lane);
-#endif
+                    for (int j = 0; j < 4; ++j) q[i][j] = acc[i][h * 4 + j];
+                gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, CE_RESID_RING, EPI>(p, q, tm * BM + wm * 128,
+                                                                            tn * BN + wn * 128 + h * 64, lane);
+            }
         }
         trace_stamp(p, 2, t * grid + blockIdx.x);
 #pragma unroll
@@ -1893,7 +1245,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         // set0 of the next tile's first K-tile (step g; its DMA was retired before the epilogue
         // and published by the last B2 barrier; its buffer is not refilled before that K-tile's B2)
-        if constexpr (NEWLOOP) read_set0(smem + (g & 1) * STAGE_BYTES);
+        read_set0(smem + (g & 1) * STAGE_BYTES);
     }
 #undef CE_MFMA_AGPR0
 #undef CE_MFMA_AGPR
@@ -1933,19 +1285,11 @@ __device__ __forceinline__ float sum_lane_groups(float v) {
 //    stores them plus the slab statistics;
 //  * the next tile waits for its K-tile 0 with vmcnt(52): the 36 stores of (e) and the 16 DMAs of
 //    K-tile 1 may stay in flight.
-// Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.
-// ABL: timing ablations (bit 0 no residual loads, bit 1 no stores; wrong outputs); bit 2: a K-tile's
-// operand DMAs spread over B2 and B3 (GEMM_VAR_W4_DMA_SPREAD); bit 4 (GEMM_VAR_RHL_EARLY67): the
-// residual of fragment rows 6-7 loaded into registers during the last K-tile's B3 (whose set-0
-// registers are free) instead of at the epilogue's start, so it is older than every store of the
-// epilogue; bit 5 (GEMM_VAR_RHL_NOREAD2): the staged-row reads as single ds_read_b64 (hipcc pairs
-// the hi / lo reads into ds_read2st64_b64, whose 32-bank 16-lane groups see a 2-way conflict on
-// this image)
-template <int ABL>
+// Requires N % 256 == 0 (the host falls back to SCHED 1 otherwise) and K >= 128.  A K-tile's
+// operand DMAs are spread over B2 (10) and B3 (6) as in SCHED 11.  (Timing ablations without residual
+// loads / stores, a store drain per tile and early rows 6-7: DESIGN.md §6.4, §6.12; removed in round 6.)
 __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
-    constexpr bool RSPREAD = (ABL & 4) != 0;
-    constexpr bool EARLY67 = (ABL & 16) != 0;
-    constexpr bool NOREAD2 = (ABL & 32) != 0;
+    constexpr bool RSPREAD = true;
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -2044,11 +1388,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
     f32x4 acc[8][8];
     bf16x8 a0[8], b0[8], a1[8], b1[8];
     u32x4 rah[8], ral[8];                       // residual of fragment rows 4-5 (hi, lo planes)
-    u32x4 rbh[8], rbl[8];                       // rows 6-7 (EARLY67: from the last K-tile's B3)
-    if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) rah[j] = ral[j] = u32x4{0u, 0u, 0u, 0u};
-    }
+    u32x4 rbh[8], rbl[8];                       // rows 6-7
 #define CE_MFMA_AGPR(ACC, BV, AV) \
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(BV), "v"(AV))
     auto read_set0 = [&](const char* sb0) __attribute__((always_inline)) {
@@ -2106,7 +1446,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 if constexpr (MODE == 0) dma_k(buf, kt + 2, s2 >> 2, voffA, voffW);
                 else dma_r(buf, MODE - 1, s2 >> 2, vr0, vr1);
             }
-            if constexpr (MODE == 1 && (ABL & 1) == 0) {
+            if constexpr (MODE == 1) {
                 if ((s2 & 3) == 1) {
                     const int q = s2 >> 2;
                     if (q < 8) rah[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdH, rpk + q * 32, n0 * 2, 0));
@@ -2114,7 +1454,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 }
             }
         }
-        if constexpr (MODE == 1 && (ABL & 1) == 0) {
+        if constexpr (MODE == 1) {
             // 16 residual DMAs + 16 register loads younger than K-tile nk - 1 (+ the previous
             // epilogue's 36 stores when nk == 2: 68 > 63, so the wait over-covers by 5)
             if (wait_n == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
@@ -2130,23 +1470,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();
-        int rpk6 = 0;
-        if constexpr (MODE == 2 && EARLY67) {
-            const int lnr = fresh_lane_id();
-            rpk6 = ((wm * 128 + 96 + (lnr & 15) + ((lnr >> 4) & 1) * 16) * (int)p.ldr + wn * 128 + (lnr >> 5) * 8) * 2;
-        }
 #pragma unroll
         for (int s2 = 0; s2 < 32; ++s2) {
             const int i = s2 >> 3, j = s2 & 7;
             CE_MFMA_AGPR(acc[4 + i][j], b1[j], a1[4 + i]);
-            if constexpr (MODE == 2 && EARLY67) {
-                // rows 6-7 of both planes, 16-B store layout (load_pair's), one load per 2 MFMAs
-                if (s2 & 1) {
-                    const int q = s2 >> 1;
-                    if (q < 8) rbh[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdH, rpk6 + q * 32, n0 * 2, 0));
-                    else rbl[q - 8] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdL, rpk6 + (q - 8) * 32, n0 * 2, 0));
-                }
-            }
             if constexpr (MODE == 0 && RSPREAD) {
                 // the other 6 DMAs of K-tile kt + 2 (buf's last reader was B1, before the first barrier)
                 if (s2 % 5 == 4) dma_k(buf, kt + 2, 10 + s2 / 5, voffA, voffW);
@@ -2216,17 +1543,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
         // a scratch reload waits for every store)
         const __amdgpu_buffer_rsrc_t hs = make_srd(p.rhl + (size_t)mbase * ldr, rows * ldr * 2);
         const __amdgpu_buffer_rsrc_t ls = make_srd(p.rhl + p.hl_plane + (size_t)mbase * ldr, rows * ldr * 2);
-        constexpr bool abl_r = (ABL & 1) != 0, abl_s = (ABL & 2) != 0;
         // a fragment-row pair (i0, i0 + 1) is loaded in the store layout (16 B = 8 columns of one
         // row per lane, half the instructions of the 8-B fragment layout) and turned into fragments
         // by the same v_permlane16_swap pairing that the stores use (an involution)
         const int rp = ((fre + (fqe & 1) * 16) * ldr + nbase + (fqe >> 1) * 8) * 2;
         auto load_pair = [&](u32x4 (&h)[8], u32x4 (&l)[8], int i0) __attribute__((always_inline)) {
-            if constexpr (abl_r) {                        // timing ablation: no residual loads
-#pragma unroll
-                for (int j = 0; j < 8; ++j) h[j] = l[j] = u32x4{0u, 0u, 0u, 0u};
-                return;
-            }
             int io = i0 * 16 * ldr * 2;
             asm volatile("" : "+s"(io));
             const int vo = rp + io;
@@ -2236,8 +1557,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 l[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ls, vo + j * 32, 0, 0));
             }
         };
-        // (a) rows 6-7 (rows 4-5 arrived with the last K-tiles; EARLY67: 6-7 too)
-        if constexpr (!EARLY67) load_pair(rbh, rbl, 6);
+        // (a) rows 6-7 (rows 4-5 arrived with the last K-tiles)
+        load_pair(rbh, rbl, 6);
         const __amdgpu_buffer_rsrc_t xs = make_srd(p.xb + (size_t)mbase * ldo, rows * ldo * 2);
         const __amdgpu_buffer_rsrc_t xl = make_srd(p.xb + p.hl_plane + (size_t)mbase * ldo, rows * ldo * 2);
         int xo = ((fre + (fqe & 1) * 16) * ldo + nbase + (fqe >> 1) * 8) * 2;
@@ -2279,10 +1600,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 const auto yy = __builtin_amdgcn_permlane16_swap(l[0].y, l[1].y, false, false);
                 const u32x4 dh = {x[0], y[0], x[1], y[1]};
                 const u32x4 dl = {xx[0], yy[0], xx[1], yy[1]};
-                if constexpr (!abl_s) {                   // (timing ablation: no stores)
-                    __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
-                }
+                __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
             }
             xo += 32 * ldo * 2;
 #pragma unroll
@@ -2309,7 +1628,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
             for (int r2 = 0; r2 < 2; ++r2) {
                 const int off = lr0 + (i0 + r2) * 16 * 512 + (c << 4) + (fqe & 1) * 8;
                 int offl = llo + off;
-                if constexpr (NOREAD2) asm volatile("" : "+v"(offl));   // keeps the two reads apart
                 const uint2 h = *reinterpret_cast<const uint2*>(smem + off);
                 const uint2 l = *reinterpret_cast<const uint2*>(smem + offl);
                 const float2 a = join_hl(h.x, l.x), b = join_hl(h.y, l.y);
@@ -2358,168 +1676,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, stb[sl]), ss, so + 64 * ns * 8 + sl * 8, 0, 0);
             }
         }
-        // ABL bit 3 (GEMM_VAR_RHL_DRAIN): every store of this epilogue retires here, so none is in
-        // flight beside the next tile's K-loop DMAs (whose waits would otherwise cover them)
-        if constexpr ((ABL & 8) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         trace_stamp(p, 2, t * grid + blockIdx.x);
     }
 #undef CE_MFMA_AGPR
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-}
-
-// ------------------------------------------------------------------------------------------
-// SCHED 12 ("w2"): TWO 256-thread workgroups per CU, each computing a 256 x 128 tile with four
-// waves of 128 x 64 (2 x 2; acc[8][4] of v_mfma_f32_16x16x32_bf16, the SCHED 1 per-wave tile and
-// epilogue layout).  72 KB of LDS per workgroup (a 3-slot ring of BK = 32 stages: A 256 x 64 B,
-// W 128 x 64 B), so two workgroups fit a CU and one's epilogue (GELU / LN fold / residual /
-// LN stats) runs beside the other's MFMAs — SCHED 1 and 11 run one workgroup per CU and leave the
-// matrix pipe idle for the whole epilogue.  Per K-step: counted vmcnt (the step after this one
-// stays in flight), one barrier, the DMA of step t+2 into the slot step t-1 used, 12 fragment
-// reads, 32 MFMAs.  LDS image: 64-B rows, 16-B chunk c of row r at c ^ (2 * ((r >> 3) & 1)) —
-// conflict-free for the four 16-lane groups of ds_read_b128 (tools/lds_bank_sim.py); the DMA
-// source address carries the inverse permutation.
-constexpr int W2_BN = 128, W2_BK = 32;
-constexpr int W2_A_BYTES = BM * W2_BK * 2;          // 16 KB
-constexpr int W2_SLOT = (BM + W2_BN) * W2_BK * 2;   // 24 KB
-constexpr int W2_NSLOT = 3;
-#ifndef CE_W2_SOLO
-#define CE_W2_SOLO 0     // diagnostic build: pad LDS so one workgroup runs per CU
-#endif
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI = EPI_PLAIN>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_w2(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[CE_W2_SOLO ? 2 * W2_NSLOT * W2_SLOT : W2_NSLOT * W2_SLOT];
-    trace_stamp(p, 0);
-    stagger_sleep(p);
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int tiles_m = (p.M + BM - 1) / BM;
-    const int tiles_n = (p.N + W2_BN - 1) / W2_BN;
-    const int nwg = tiles_m * tiles_n;
-    const int wgid = xcd_remap(blockIdx.x, nwg);
-    int tm, tn;
-    tile_of(wgid, tiles_m, tiles_n, p.gm, tm, tn);
-    const int m0 = tm * BM, n0 = tn * W2_BN;
-    const int nk = p.K / W2_BK;
-
-    // staging: instruction j (0..5) of wave w moves 16 rows x 64 B; j < 4: A rows 16(4j+w) + (lane>>2),
-    // else W rows 16(4(j-4)+w) + (lane>>2); LDS chunk lane&3 holds source chunk (lane&3) ^ f(row)
-    const int srow = lane >> 2;
-    const int schunk = (lane & 3) ^ (((lane >> 5) & 1) << 1);
-    const __amdgpu_buffer_rsrc_t srdA = make_srd(p.A + (size_t)m0 * p.lda, max(0, min(p.M - m0, BM)) * (int)p.lda * 2);
-    const __amdgpu_buffer_rsrc_t srdW =
-        make_srd(p.W + (size_t)n0 * p.ldw, max(0, min(p.N - n0, W2_BN)) * (int)p.ldw * 2);
-    int voff[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const int g = j < 4 ? 4 * j + wave : 4 * (j - 4) + wave;
-        const int row = 16 * g + srow;
-        voff[j] = row * (int)(j < 4 ? p.lda : p.ldw) * 2 + schunk * 16;
-    }
-    auto dma = [&](int kt) {
-        char* base = smem + (kt % W2_NSLOT) * W2_SLOT;
-        const int kb = kt * W2_BK * 2;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const int g = j < 4 ? 4 * j + wave : 4 * (j - 4) + wave;
-            if (j < 4)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(base + g * 1024), 16, voff[j], kb, 0, 0);
-            else
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(base + W2_A_BYTES + g * 1024), 16,
-                                                         voff[j], kb, 0, 0);
-        }
-    };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int fo = fr * 64 + ((fq ^ (((fr >> 3) & 1) << 1)) << 4);
-    const int a_off = wm * 128 * 64 + fo;
-    const int w_off = W2_A_BYTES + wn * 64 * 64 + fo;
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // Two phases per K-step t, one barrier each:
-    //   A: MFMA rows 0-3 (alo, b[t])   | reads ahi (rows 4-7) of t, DMA of step t+2
-    //      lgkmcnt(0), vmcnt(step t+1 landed), barrier
-    //   B: MFMA rows 4-7 (ahi, b[t])   | reads alo and b of step t+1
-    // The DMA of step t+2 goes into the slot of step t-1, whose last reads (ahi in phase A of t-1)
-    // retired before that phase's barrier.  b is double-buffered (bx / by by the parity of t).
-    bf16x8 alo[4], ahi[4], bx[4], by[4];
-    auto rd = [&](bf16x8 (&d)[4], const char* sb, int off, int i0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = *reinterpret_cast<const bf16x8*>(sb + off + (i0 + q) * 16 * 64);
-    };
-    auto slot = [&](int kt) { return smem + (kt % W2_NSLOT) * W2_SLOT; };
-    auto mf = [&](int i0, const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i0 + i][j], 0, 0, 0);
-    };
-    auto step = [&](int kt, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
-        const char* sb = slot(kt);
-        // ---- phase A ----
-        mf(0, alo, bc);
-        rd(ahi, sb, a_off, 4);
-        const bool pf = kt + 2 < nk;
-        if (pf) dma(kt + 2);
-#pragma unroll
-        for (int g2 = 0; g2 < 4; ++g2) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-#pragma unroll
-        for (int g2 = 0; g2 < 6; ++g2) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (pf) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- phase B ----
-        mf(4, ahi, bc);
-        if (kt + 1 < nk) {
-            const char* sn = slot(kt + 1);
-            rd(bn, sn, w_off, 0);
-            rd(alo, sn, a_off, 0);
-        }
-#pragma unroll
-        for (int g2 = 0; g2 < 8; ++g2) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    dma(0);
-    if (nk > 1) {
-        dma(1);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();
-    rd(bx, smem, w_off, 0);
-    rd(alo, smem, a_off, 0);
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-        step(kt, bx, by);
-        step(kt + 1, by, bx);
-    }
-    if (kt < nk) step(kt, bx, by);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    trace_stamp(p, 1);
-    gemm_epilogue<ACT, HAS_RESID, OUT_BF16, 4, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>(
-        p, acc, m0 + wm * 128, n0 + wn * 64, lane);
-    trace_stamp(p, 2);
 }
 
 // Process-wide A/B knobs (knobs.h: atomics, env value published by the first reader)
@@ -2527,31 +1687,31 @@ std::atomic<int> g_variant{kKnobUnset};
 int variant_env() { const int v = env_int("CE_GEMM_VARIANT", CE_GEMM_VAR_DEFAULT); return v < 0 ? 0 : v; }
 int gemm_variant() { return knob_get(g_variant, variant_env); }
 
-bool sched_ok(int sc) {
-    return sc == 0 || sc == 1 || sc == 2 || sc == 3 || sc == 4 || sc == 6 || sc == 7 || sc == 9 || sc == 10 ||
-           sc == 11 || sc == 12 || sc == 13 || sc == 14;
-}
+// Main-loop schedule: 1 = the default shape policy (SCHED 1 / the four-wave kernels by shape), 11 = the
+// four-wave persistent kernel wherever its epilogues apply.
+bool sched_ok(int sc) { return sc == 1 || sc == 11; }
+// The schedule knobs in ONE atomic word, so a launch never sees a half-applied ce_set_gemm_schedule:
+// bits 0-7 schedule, 8-15 tile-order M-group, 16-30 first-round stagger (units of s_sleep 127).
+constexpr int pack_sched(int sc, int gm, int st) { return sc | (gm << 8) | (st << 16); }
 std::atomic<int> g_sched{kKnobUnset};
-std::atomic<int> g_ring{CE_RESID_RING};     // residual prefetch ring depth of SCHED 1 (2..5; A/B only)
-// diagnostic timeline buffer (ce_set_gemm_trace): process-wide by contract (clipembed.h)
-std::atomic<unsigned long long*> g_trace{nullptr};
-std::atomic<long> g_trace_n{0};
-std::atomic<int> g_stagger{kKnobUnset};     // first-round de-synchronisation sleep (units of s_sleep 127)
-int stagger_env() { return std::max(0, env_int("CE_GEMM_STAGGER", 0)); }
-int gemm_stagger() { return knob_get(g_stagger, stagger_env); }
-int sched_env() { const int s = env_int("CE_GEMM_SCHED", 1); return sched_ok(s) ? s : 1; }
-int gemm_sched() { return knob_get(g_sched, sched_env); }
+int sched_env() {
+    const int sc = env_int("CE_GEMM_SCHED", 1), g = env_int("CE_GEMM_GROUPM", 4);
+    const int st = std::max(0, std::min(env_int("CE_GEMM_STAGGER", 0), 0x7fff));
+    return pack_sched(sched_ok(sc) ? sc : 1, (g < 1 || g > 64) ? 1 : g, st);
+}
+int gemm_sched_word() { return knob_get(g_sched, sched_env); }
+// diagnostic timeline buffer (ce_set_gemm_trace): process-wide by contract (clipembed.h); pointer and
+// size change together under the lock and a launch reads them together
+struct TraceBuf { unsigned long long* buf = nullptr; long n = 0; };
+TraceBuf g_trace;
+std::mutex g_trace_mu;
 
 int num_cus() { return device_cus(); }
 
-std::atomic<int> g_groupm{kKnobUnset};
-int groupm_env() { const int g = env_int("CE_GEMM_GROUPM", 4); return (g < 1 || g > 64) ? 1 : g; }
-int gemm_groupm() { return knob_get(g_groupm, groupm_env); }
-
 // Split-K tail plan: with one 512-thread workgroup per CU, a grid of T tiles runs in ceil(T / CUs)
-// rounds; when the last round holds only R = T % CUs tiles (vision out-proj / c_proj at B = 256:
-// 2308 tiles = 9 rounds + 4 tiles) the chip idles for most of a tile time.  Those R tiles are split
-// into S K-chunks (R * S <= CUs) so the last round is ~1/S of a tile, plus a tiny fixup launch.
+// rounds; when the last round holds only R = T % CUs tiles the chip idles for most of a tile time.
+// Those R tiles are split into S K-chunks (R * S <= CUs) so the last round is ~1/S of a tile, plus a
+// tiny fixup launch.
 std::atomic<int> g_splitk{kKnobUnset};
 int splitk_env() { return env_int("CE_GEMM_SPLITK", 1) != 0; }
 bool splitk_enabled() { return knob_get(g_splitk, splitk_env) != 0; }
@@ -2598,11 +1758,21 @@ float* kernel_api_part() {
     return g_part[dev];
 }
 
-// the four-wave epilogue written for one wave per SIMD (bf16 out, no residual)
-template <bool HAS_RESID, bool OUT_BF16, int EPI>
-bool w4_epi2(const GemmParams& p) {
-    if constexpr (OUT_BF16 && !HAS_RESID && EPI != EPI_LN_STATS) return (p.variant & GEMM_VAR_W4_EPI2) != 0;
-    else if constexpr (EPI == EPI_LN_STATS) return (p.variant & GEMM_VAR_W4_EPI2) != 0 && p.grp == 0;
+// The epilogues the four-wave persistent kernel has: bf16 without residual (plain / LN fold; the
+// one-wave-per-SIMD epilogue, GEMM_VAR_W4_EPI2), the f32 LN-statistics residual (EPI2, identity row
+// map), and a plain f32 output without residual or activation (the generic register epilogue: the
+// PACL head's linear branch)
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
+constexpr bool w4_has() {
+    return (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD)) ||
+           (EPI == EPI_LN_STATS && HAS_RESID && !OUT_BF16) || (!OUT_BF16 && !HAS_RESID && EPI == EPI_PLAIN && ACT == ACT_NONE);
+}
+template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
+bool w4_ok(const GemmParams& p) {
+    if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
+        return (p.variant & GEMM_VAR_W4_EPI2) != 0;
+    else if constexpr (EPI == EPI_LN_STATS && HAS_RESID && !OUT_BF16) return (p.variant & GEMM_VAR_W4_EPI2) != 0 && p.grp == 0;
+    else if constexpr (!OUT_BF16 && !HAS_RESID && EPI == EPI_PLAIN && ACT == ACT_NONE) return true;
     else return false;
 }
 
@@ -2610,7 +1780,7 @@ bool w4_epi2(const GemmParams& p) {
 // holds r <= grid / 8 tiles idles most of the chip for a whole tile; the persistent kernel runs the
 // whole rounds only, and those r tiles follow as S K-chunks (about 4 K-tiles each, r * S <= grid) on
 // the 4-phase kernel in tail-only mode, summed and finished by gemm_splitk_fixup (vision QKV
-// 6924 = 27 * 256 + 12 tiles, c_fc 9232 = 36 * 256 + 16).
+// 6924 = 27 * 256 + 12 tiles, c_fc 9232 = 36 * 256 + 16).  Off by default (GEMM_VAR_W4_TAIL).
 void plan_tail_w4(GemmParams& p, int nwg, int grid) {
     p.tail = 0;
     p.split = 1;
@@ -2652,7 +1822,8 @@ int w4pp_grid(const GemmParams& p, int nwg, bool onetile = false) {
 // Shape policy of the default schedule (CE_GEMM_AUTO, default 1): SCHED 11 for large grids
 // (>= 4 tiles per CU) without a residual — the vision QKV and c_fc GEMMs, plain or LN-folded, with
 // or without GELU — when its one-wave-per-SIMD epilogue (GEMM_VAR_W4_EPI2) is on; otherwise only
-// the no-activation ones (the round-1 policy).  Residual epilogues (out-proj / c_proj) stay on
+// the no-activation ones (the round-1 policy).  The hi/lo residual GEMMs (out-proj / c_proj) run on
+// their own staged-residual four-wave kernel (launch_epi); the f32-stream residual epilogues stay on
 // SCHED 1: on the persistent grid vmcnt retires the epilogue's stores and the next tile's DMAs in
 // issue order, so their 384 KB per tile must drain within two K-tiles (r02 A/B: out-proj 572 vs
 // 593 TF/s, c_proj 1037 vs 1025; with the stores ablated 855 / 1204, profiles/r02).
@@ -2680,7 +1851,6 @@ bool auto_w4pp(const GemmParams& p, int act, bool resid) {
 std::atomic<long long> g_path[GEMM_PATH_COUNT];
 inline void count_path(int path) { g_path[path].fetch_add(1, std::memory_order_relaxed); }
 
-// LN-fold / LN-stats epilogues exist for SCHED 1 and SCHED 11
 // SCHED 1 (one workgroup per CU): half the CUs of every XCD (bit 3 of the block id: blocks b and
 // b + 8 share an XCD) start their first tile late
 void set_stagger_1(GemmParams& p, int nwg) {
@@ -2691,55 +1861,33 @@ void set_stagger_1(GemmParams& p, int nwg) {
     p.stagger_bit = 3;
 }
 
-// SCHED 13 (gemm_db.hip): bf16 output without residual, whole 128-column tiles, >= 16 K-tiles, full rows
+// The four-wave persistent kernel (+ its optional split-K tail on the 4-phase kernel)
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
-bool db_ok(const GemmParams& p) {
-    if constexpr (!OUT_BF16 || HAS_RESID || !(EPI == EPI_PLAIN || EPI == EPI_LN_FOLD)) return false;
-    else return p.kn.sched == 13 && p.N % 128 == 0 && p.K >= 16 * BK && !p.m_dev && !p.onetile && p.grp == 0;
-}
-
-template <int ACT, int EPI>
-hipError_t launch_db(const GemmParams& p0, hipStream_t s) {
-    GemmParams p = p0;
+hipError_t launch_w4pp(GemmParams& p, hipStream_t s) {
     p.gm = p.kn.groupm;
-    p.tail = 0;
-    p.split = 1;
-    const int nwg = ((p.M + BM - 1) / BM) * (p.N / 128);
-    count_path(GEMM_PATH_OTHER);
-    return launch_gemm_db(p, ACT, EPI, w4pp_grid(p, nwg), s);
-}
-
-template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
-hipError_t launch_w2(const GemmParams& p0, hipStream_t s) {
-    GemmParams p = p0;
-    p.gm = p.kn.groupm;
-    p.tail = 0;
-    p.split = 1;
-    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + W2_BN - 1) / W2_BN);
-    if (nwg > 2 * num_cus()) {     // the second workgroup of each CU starts half a tile late
-        p.stagger = p.kn.stagger;
-        p.stagger_lo = num_cus();
-        p.stagger_hi = 2 * num_cus();
-        p.stagger_bit = -1;
+    p.stagger = p.kn.stagger;
+    const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+    const int grid = w4pp_grid(p, nwg, p.onetile);
+    plan_tail_w4(p, nwg, grid);
+    if (p.pre_out && p.tail > 0) return hipErrorInvalidValue;     // the tail kernel has no pre_out store
+    hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(grid), dim3(256), 0, s, p);
+    count_path(GEMM_PATH_W4PP + EPI);
+    if (p.tail > 0) {
+        GemmParams q = p;
+        q.tail_only = 1;
+        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
+                           dim3(p.tail * p.split), dim3(NTHREADS), 0, s, q);
+        hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
+        count_path(GEMM_PATH_FIXUP + EPI);
     }
-    hipLaunchKernelGGL((gemm_bf16_w2<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(nwg), dim3(256), 0, s, p);
-    count_path(GEMM_PATH_W2 + EPI);
     return hipGetLastError();
 }
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16, int EPI>
 hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
-    // the hi/lo residual epilogues exist on SCHED 1 (+ its split-K tail) only
     constexpr bool HL = EPI == EPI_LN_STATS_HL || EPI == EPI_HL_F32;
     if constexpr (EPI == EPI_LN_STATS_HL) {
-        const bool w2b_pol = p.kn.sched == 1 && p.kn.autom != 0 &&
-                             ((p.variant & GEMM_VAR_W2B_RESID) || ((p.variant & GEMM_VAR_W2B_OUT) && p.K <= 2048));
-        if ((p.kn.sched == 14 || w2b_pol) && !p.onetile && gemm_w2b_supported(p, EPI, false, false)) {
-            p.gm = p.kn.groupm;
-            count_path(GEMM_PATH_W2 + EPI_LN_STATS);
-            return launch_gemm_w2b(p, ACT_NONE, EPI, s);
-        }
         // staged-residual four-wave kernel (default policy): whole 256-column tiles, >= 2 K-tiles,
         // a grid of >= 2 tiles per CU (no split-K tail); CE_GEMM_AUTO=0 or a pinned schedule keeps
         // SCHED 1 (r02 A/B at B = 256: out-proj 682 vs 589 TF/s, c_proj 1,092 vs 995)
@@ -2748,28 +1896,14 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             p.K >= 2 * BK && (nwg >= 2 * num_cus() || p.onetile)) {
             p.gm = p.kn.groupm;
             p.stagger = p.kn.stagger;
-            plan_tail_rhl(p, nwg, w4pp_grid(p, nwg, p.onetile));
-            const int abl = ((p.variant & GEMM_VAR_ABL_NORESID) ? 1 : 0) | ((p.variant & GEMM_VAR_ABL_NOSTORE) ? 2 : 0);
-            const int ex = ((p.variant & GEMM_VAR_RHL_EARLY67) ? 16 : 0) | ((p.variant & GEMM_VAR_RHL_NOREAD2) ? 32 : 0);
-            if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 16)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<20>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 32)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<36>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && ex == 48)
-                hipLaunchKernelGGL(gemm_w4_resid_hl<52>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD) && (p.variant & GEMM_VAR_RHL_DRAIN))
-                hipLaunchKernelGGL(gemm_w4_resid_hl<12>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0 && (p.variant & GEMM_VAR_RHL_DMA_SPREAD))
-                hipLaunchKernelGGL(gemm_w4_resid_hl<4>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 0) hipLaunchKernelGGL(gemm_w4_resid_hl<0>, dim3(w4pp_grid(p, nwg, p.onetile)), dim3(256), 0, s, p);
-            else if (abl == 1) hipLaunchKernelGGL(gemm_w4_resid_hl<1>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
-            else if (abl == 2) hipLaunchKernelGGL(gemm_w4_resid_hl<2>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
-            else hipLaunchKernelGGL(gemm_w4_resid_hl<3>, dim3(w4pp_grid(p, nwg)), dim3(256), 0, s, p);
+            const int grid = w4pp_grid(p, nwg, p.onetile);
+            plan_tail_rhl(p, nwg, grid);
+            hipLaunchKernelGGL(gemm_w4_resid_hl, dim3(grid), dim3(256), 0, s, p);
             count_path(GEMM_PATH_W4PP + EPI_LN_STATS);
             if (p.tail > 0) {
                 GemmParams q = p;
                 q.tail_only = 1;
-                hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, true, false, 1, 3, EPI_LN_STATS_HL>), dim3(p.tail * p.split),
+                hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, true, false, 3, EPI_LN_STATS_HL>), dim3(p.tail * p.split),
                                    dim3(NTHREADS), 0, s, q);
                 hipLaunchKernelGGL((gemm_splitk_fixup<ACT_NONE, true, false, EPI_LN_STATS_HL>), dim3(p.tail * 64),
                                    dim3(256), 0, s, p);
@@ -2778,49 +1912,9 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
             return hipGetLastError();
         }
     }
-    if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
-        if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p)) return launch_db<ACT, EPI>(p, s);
-    if constexpr (OUT_BF16 && !HAS_RESID && (EPI == EPI_PLAIN || EPI == EPI_LN_FOLD))
-        if ((p.kn.sched == 14 || (EPI == EPI_LN_FOLD && p.kn.sched == 1 && p.kn.autom != 0 &&
-                                  (p.variant & GEMM_VAR_W2B_FOLD) && !p.m_dev)) &&
-            !p.onetile && gemm_w2b_supported(p, EPI, true, false)) {
-            p.gm = p.kn.groupm;
-            count_path(GEMM_PATH_W2 + EPI);
-            return launch_gemm_w2b(p, ACT, EPI, s);
-        }
-    if (!HL && p.kn.sched == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
-    if (!HL && (p.kn.sched == 11 || auto_w4pp(p, ACT, HAS_RESID))) {
-        p.gm = p.kn.groupm;
-        p.stagger = p.kn.stagger;
-        const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-        const int grid = w4pp_grid(p, nwg, p.onetile);
-        plan_tail_w4(p, nwg, grid);
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-            (p.variant & GEMM_VAR_W4_SPREAD12))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 7>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (p.variant & GEMM_VAR_W4_SPREAD8))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 11>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (p.variant & GEMM_VAR_W4_SPREAD_EVEN))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 19>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 3>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI>(p))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI, 1>), dim3(grid), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(grid), dim3(256), 0, s, p);
-        count_path(GEMM_PATH_W4PP + EPI);
-        if (p.tail > 0) {
-            GemmParams q = p;
-            q.tail_only = 1;
-            hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, EPI == EPI_LN_STATS ? 3 : CE_RESID_RING, EPI>),
-                               dim3(p.tail * p.split), dim3(NTHREADS), 0, s, q);
-            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16, EPI>), dim3(p.tail * 64), dim3(256), 0, s, p);
-            count_path(GEMM_PATH_FIXUP + EPI);
-        }
-        return hipGetLastError();
-    }
+    if constexpr (!HL && w4_has<ACT, HAS_RESID, OUT_BF16, EPI>())
+        if ((p.kn.sched == 11 || auto_w4pp(p, ACT, HAS_RESID)) && w4_ok<ACT, HAS_RESID, OUT_BF16, EPI>(p))
+            return launch_w4pp<ACT, HAS_RESID, OUT_BF16, EPI>(p, s);
     p.gm = p.kn.groupm;
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
     p.tail = 0;
@@ -2830,7 +1924,7 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
     constexpr int RG = (EPI == EPI_LN_STATS || EPI == EPI_LN_STATS_HL) ? 3 : CE_RESID_RING;
     // path counters: the hi/lo epilogues count as their f32-stream counterparts
     constexpr int CNT = EPI == EPI_LN_STATS_HL ? EPI_LN_STATS : EPI == EPI_HL_F32 ? EPI_PLAIN : EPI;
-    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, RG, EPI>), dim3(nwg - p.tail + p.tail * p.split),
+    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, RG, EPI>), dim3(nwg - p.tail + p.tail * p.split),
                        dim3(NTHREADS), 0, s, p);
     count_path(GEMM_PATH_NT + CNT);
     if (p.tail > 0) {
@@ -2843,8 +1937,8 @@ hipError_t launch_epi(const GemmParams& p0, hipStream_t s) {
 // The pre-activation copy (GemmParams::pre_out) is written only by the four-wave persistent kernel's
 // one-wave-per-SIMD bf16 epilogue (w4_epilogue_bf16_n, EPI_PLAIN with an activation) over every tile:
 // no split-K tail (its tiles run on SCHED 1, which has no pre_out store), no one-tile grid.
-// launch_gemm routes pre_out launches through here only when this holds, and launch_t rejects any
-// launch whose chosen path would leave pre_out unwritten (the backward would read stale values).
+// launch_gemm routes pre_out launches through here only when this holds, and launch_w4pp rejects
+// a launch whose plan would leave pre_out unwritten (the backward would read stale values).
 bool pre_out_fused(const GemmParams& p, int act) {
     return act != ACT_NONE && !p.onetile && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
            !(p.variant & GEMM_VAR_W4_TAIL);
@@ -2852,118 +1946,52 @@ bool pre_out_fused(const GemmParams& p, int act) {
 
 // knobs of one launch (launch_gemm's snapshot, GemmParams::kn)
 void snapshot_knobs(GemmParams& p) {
-    p.trace = g_trace;
-    p.trace_n = (int)std::min<long>(g_trace_n, 1 << 30);
+    {
+        std::lock_guard<std::mutex> lk(g_trace_mu);
+        p.trace = g_trace.buf;
+        p.trace_n = (int)std::min<long>(g_trace.n, 1 << 30);
+    }
     p.variant = gemm_variant();
-    p.kn.sched = gemm_sched();
+    const int sw = gemm_sched_word();
+    p.kn.sched = sw & 0xff;
+    p.kn.groupm = (sw >> 8) & 0xff;
+    p.kn.stagger = (sw >> 16) & 0x7fff;
     p.kn.autom = gemm_auto();
     p.kn.splitk = splitk_enabled() ? 1 : 0;
-    p.kn.groupm = gemm_groupm();
-    p.kn.stagger = gemm_stagger();
-    p.kn.ring = g_ring.load();
+    p.kn.snap = 1;
     p.onetile = (p.onetile && (p.variant & GEMM_VAR_SMALL_ONETILE)) ? 1 : 0;
 }
 
-// The activation-backward epilogue exists on the four-wave persistent kernel with the default
-// variant bits' DMA split (EV 3) only, without a split-K tail, for whole 128-column quadrants.
+// The activation-backward epilogue exists on the four-wave persistent kernel only, without a split-K
+// tail, for whole 128-column quadrants.
 bool act_bwd_fused_k(const GemmParams& p, int act) {
-    const int spread_alt = GEMM_VAR_W4_SPREAD12 | GEMM_VAR_W4_SPREAD8 | GEMM_VAR_W4_SPREAD_EVEN;
     return (act == ACT_GELU || act == ACT_QGELU) && p.bwd_pre && p.bwd_part && p.out && !p.bias && !p.resid &&
            !p.rhl && !p.pre_out && !p.m_dev && !p.grp && !p.onetile && p.M > 0 && p.ldo == p.N && p.N % 128 == 0 &&
            p.K > 0 && p.K % BK == 0 && auto_w4pp(p, act, false) && (p.variant & GEMM_VAR_W4_EPI2) &&
-           (p.variant & GEMM_VAR_W4_DMA_SPREAD) && !(p.variant & spread_alt) && !(p.variant & GEMM_VAR_W4_TAIL);
+           !(p.variant & GEMM_VAR_W4_TAIL);
 }
 
 template <int ACT, bool HAS_RESID, bool OUT_BF16>
 hipError_t launch_t(const GemmParams& p0, hipStream_t s) {
     GemmParams p = p0;
+    if (p.pre_out && !(OUT_BF16 && !HAS_RESID && pre_out_fused(p, ACT))) return hipErrorInvalidValue;
+    if constexpr (w4_has<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>())
+        if ((p.kn.sched == 11 || auto_w4pp(p, ACT, HAS_RESID)) && w4_ok<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
+            return launch_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
+    if (p.pre_out) return hipErrorInvalidValue;
     p.gm = p.kn.groupm;
     const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-    if (p.pre_out && !(OUT_BF16 && !HAS_RESID && pre_out_fused(p, ACT))) return hipErrorInvalidValue;
-    if constexpr (OUT_BF16 && !HAS_RESID)
-        if (db_ok<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p)) return launch_db<ACT, EPI_PLAIN>(p, s);
-    if constexpr (OUT_BF16 && !HAS_RESID)
-        if (p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, EPI_PLAIN, true, false)) {
-            count_path(GEMM_PATH_W2);
-            return launch_gemm_w2b(p, ACT, EPI_PLAIN, s);
-        }
-    const int sc = auto_w4pp(p, ACT, HAS_RESID) ? 11 : p.kn.sched;
-    if (sc == 12) return launch_w2<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN>(p, s);
     p.tail = 0;
     p.split = 1;
-    if (sc == 1) set_stagger_1(p, nwg);
-    if (sc == 1) {
-        plan_tail(p, nwg);
-        if (p.tail > 0) {
-            const int grid = nwg - p.tail + p.tail * p.split;
-            if (HAS_RESID && p.kn.ring == 2)
-                hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(grid), dim3(NTHREADS), 0, s, p);
-            else
-                hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(grid), dim3(NTHREADS), 0, s, p);
-            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
-            count_path(GEMM_PATH_NT);
-            count_path(GEMM_PATH_FIXUP);
-            return hipGetLastError();
-        }
+    set_stagger_1(p, nwg);
+    plan_tail(p, nwg);
+    hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16>), dim3(nwg - p.tail + p.tail * p.split),
+                       dim3(NTHREADS), 0, s, p);
+    count_path(GEMM_PATH_NT);
+    if (p.tail > 0) {
+        hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
+        count_path(GEMM_PATH_FIXUP);
     }
-    count_path(sc == 11 ? GEMM_PATH_W4PP : sc == 1 ? GEMM_PATH_NT : GEMM_PATH_OTHER);
-    if (sc == 9) {
-        // one workgroup per CU (a multiple of 8 so every XCD group is complete)
-        int grid = (num_cus() / 8) * 8;
-        const int need = ((nwg + 7) / 8) * 8;
-        grid = grid < need ? grid : need;
-        hipLaunchKernelGGL((gemm_bf16_persist<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(NTHREADS), 0, s, p);
-    } else if (sc == 11) {
-        p.stagger = p.kn.stagger;
-        const int grid = w4pp_grid(p, nwg, p.onetile);
-        plan_tail_w4(p, nwg, grid);
-        if (p.pre_out && (p.tail > 0 || !w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))) return hipErrorInvalidValue;
-        if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-            (p.variant & GEMM_VAR_W4_SPREAD12))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 7>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (p.variant & GEMM_VAR_W4_SPREAD8))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 11>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD) &&
-                 (p.variant & GEMM_VAR_W4_SPREAD_EVEN))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 19>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p) && (p.variant & GEMM_VAR_W4_DMA_SPREAD))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
-        else if (w4_epi2<HAS_RESID, OUT_BF16, EPI_PLAIN>(p))
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16, EPI_PLAIN, 1>), dim3(grid), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((gemm_bf16_w4pp<ACT, HAS_RESID, OUT_BF16>), dim3(grid), dim3(256), 0, s, p);
-        if (p.tail > 0) {
-            GemmParams q = p;
-            q.tail_only = 1;
-            hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(p.tail * p.split), dim3(NTHREADS), 0, s, q);
-            hipLaunchKernelGGL((gemm_splitk_fixup<ACT, HAS_RESID, OUT_BF16>), dim3(p.tail * 64), dim3(256), 0, s, p);
-            count_path(GEMM_PATH_FIXUP);
-        }
-    } else if (sc == 10)
-        hipLaunchKernelGGL((gemm_bf16_w4p<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
-    else if (sc == 2)
-        hipLaunchKernelGGL((gemm_bf16_w4<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(256), 0, s, p);
-    else if (sc == 0)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 0>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && p.kn.ring == 2)   // residual prefetch-depth A/B (bench_kernels)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 2>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && p.kn.ring == 3)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 3>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1 && HAS_RESID && p.kn.ring == 5)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1, 5>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 1)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (sc == 6)
-        hipLaunchKernelGGL((gemm_bf16_early<ACT, HAS_RESID, OUT_BF16>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 3)   // timing ablations (qkv shape only)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 3>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 4)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 4>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else if (ACT == ACT_NONE && !HAS_RESID && OUT_BF16 && sc == 7)
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT_NONE, false, true, 7>), dim3(nwg), dim3(NTHREADS), 0, s, p);
-    else
-        hipLaunchKernelGGL((gemm_bf16_nt<ACT, HAS_RESID, OUT_BF16, 1>), dim3(nwg), dim3(NTHREADS), 0, s, p);
     return hipGetLastError();
 }
 
@@ -3000,42 +2028,46 @@ float* gemm_kernel_api_workspace(long* elems) {
 }
 
 int set_gemm_schedule(int v) {
-    const int prev = gemm_sched() | (gemm_groupm() << 8);
-    const int sc = v & 0xff, gm = (v >> 8) & 0xff, ring = (v >> 16) & 0xff, st = (v >> 24) & 0x7f;
-    if (ring >= 2 && ring <= 5) g_ring = ring;
-    if (st) g_stagger = st - 1;
-    g_sched = sched_ok(sc) ? sc : 1;
-    if (gm) g_groupm = gm <= 64 ? gm : 1;
-    return prev;
+    // one read-modify-write of the packed word: schedule (bits 0-7; other values select 1), M-group
+    // (8-15, 0 keeps it), stagger + 1 (24-30, 0 keeps it)
+    int cur = gemm_sched_word();
+    for (;;) {
+        const int sc = v & 0xff, gm = (v >> 8) & 0xff, st = (v >> 24) & 0x7f;
+        const int nsc = sched_ok(sc) ? sc : 1;
+        const int ngm = gm ? (gm <= 64 ? gm : 1) : (cur >> 8) & 0xff;
+        const int nst = st ? st - 1 : (cur >> 16) & 0x7fff;
+        if (g_sched.compare_exchange_weak(cur, pack_sched(nsc, ngm, nst), std::memory_order_acq_rel))
+            return cur & 0xffff;
+    }
 }
 
-int current_gemm_sched() { return gemm_sched(); }
+int current_gemm_sched() { return gemm_sched_word() & 0xff; }
 
 void set_gemm_trace(unsigned long long* buf, long n) {
-    g_trace = buf;
-    g_trace_n = buf ? n : 0;
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    g_trace.buf = buf;
+    g_trace.n = buf ? n : 0;
 }
 
-bool gemm_act_bwd_fused(const GemmParams& p0, int act) {
-    GemmParams p = p0;
+bool gemm_act_bwd_fused(GemmParams& p, int act) {
     snapshot_knobs(p);
     return act_bwd_fused_k(p, act);
 }
 
 hipError_t launch_gemm_act_bwd(const GemmParams& p0, int act, hipStream_t s) {
     GemmParams p = p0;
-    snapshot_knobs(p);
+    if (!p.kn.snap) snapshot_knobs(p);      // (gemm_act_bwd_fused's snapshot otherwise: one decision)
     if (!act_bwd_fused_k(p, act)) return hipErrorNotSupported;
     p.gm = p.kn.groupm;
     p.stagger = p.kn.stagger;
     const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
     const int grid = w4pp_grid(p, nwg);
     plan_tail_w4(p, nwg, grid);
-    if (p.tail) return hipErrorNotSupported;      // (W4_TAIL is off: unreachable)
+    if (p.tail) return hipErrorNotSupported;      // (W4_TAIL excluded by act_bwd_fused_k: unreachable)
     if (act == ACT_GELU)
-        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_GELU_BWD, false, true, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_GELU_BWD, false, true, EPI_PLAIN>), dim3(grid), dim3(256), 0, s, p);
     else
-        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_QGELU_BWD, false, true, EPI_PLAIN, 3>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((gemm_bf16_w4pp<ACT_QGELU_BWD, false, true, EPI_PLAIN>), dim3(grid), dim3(256), 0, s, p);
     count_path(GEMM_PATH_W4PP + EPI_PLAIN);
     return hipGetLastError();
 }
@@ -3054,9 +2086,7 @@ hipError_t launch_gemm(const GemmParams& p0, int act, bool out_bf16, hipStream_t
         p.part_elems = 0;
     }
     const bool res = p.resid != nullptr;
-    // SCHED 14 steps K by 32: it takes K % 64 == 32 too (every other path needs K % 64 == 0)
-    const bool w2b_k = p.kn.sched == 14 && !p.onetile && gemm_w2b_supported(p, epi, out_bf16, res);
-    if ((p.K % BK != 0 && !w2b_k) || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
+    if (p.K % BK != 0 || p.N % 64 != 0 || p.K <= 0) return hipErrorInvalidValue;
     if (p.pre_out) {
         // pre-activation copy: written by the four-wave kernel's one-wave-per-SIMD epilogue (the
         // default policy's path for this GEMM); on any other path the GEMM writes pre and the

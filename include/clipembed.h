@@ -282,10 +282,14 @@ int ce_kernel_stats(ce_handle* h, int index, char* name, int name_len, double* t
  * act: 0 none, 1 GELU(erf), 2 QuickGELU.  (ResidualAttentionBlock linears, transformer.py:228-239) */
 int ce_kernel_gemm_bf16(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                         int act, const float* resid, void* out, int out_dtype);
-/* Select the GEMM main-loop schedule for subsequent launches (bits 0-7: 0 = 2-stage whole-tile
- * ring, 1 = 4-phase half-tile ring, the default; bits 8-15: tile-order M-group, 0 = keep; bits 24-30:
- * 1 + first-round stagger in units of s_sleep 127 (~8k cycles) for half the CUs, 0 = keep);
- * returns the previous value in the same encoding.  For A/B measurement. */
+/* Select the GEMM main-loop schedule for subsequent launches (bits 0-7: 1 = the default shape policy
+ * (ce_set_gemm_auto: the 4-phase kernel, SCHED 1, or the four-wave persistent kernels by shape), 11 =
+ * the four-wave persistent kernel (SCHED 11) wherever its epilogues apply (bf16 without residual,
+ * f32 LN statistics, plain f32), other values select 1; bits 8-15: tile-order M-group, 0 = keep;
+ * bits 24-30: 1 + first-round stagger in units of s_sleep 127 (~8k cycles) for half the CUs, 0 =
+ * keep).  The fields change together (one atomic word).  Returns the previous schedule | M-group << 8.
+ * For A/B measurement.  (The other schedules of rounds 1-5 were measured slower and removed in
+ * round 6) */
 int ce_set_gemm_schedule(int schedule);
 /* Split-K tail of the GEMM (default on): when a grid's last round holds few tiles, those tiles are
  * computed as K-chunks summed by a fixup launch.  Returns the previous setting.  For A/B. */
@@ -297,36 +301,25 @@ int ce_set_gemm_splitk(int enable);
  * Runtime A/B of the bench configuration against the plain path in one process (parity tests). */
 int ce_set_gemm_auto(int mode);
 /* GEMM kernel-variant bits for A/B measurement (env CE_GEMM_VARIANT at first use; a negative value
- * restores the default, bits 0|1|7|8|9): bit 0 = the four-wave persistent schedule does not drain an
- * epilogue's stores at the next tile's first K-tile; bit 1 = its epilogue written for one wave per
+ * restores the default, bits 0|1|7|8|9|13): bit 0 = the four-wave persistent schedule does not drain
+ * an epilogue's stores at the next tile's first K-tile; bit 1 = its epilogues written for one wave per
  * SIMD (operands staged in LDS, clipped buffer stores; also lets the default policy put GELU GEMMs on
- * that schedule); bits 2, 3, 6 = timing ablations of the LN-statistics epilogues (no residual loads /
- * no stores / no bf16 copy: wrong outputs); bit 4 = one tile per four-wave workgroup; bit 5 = split-K
- * tail on the four-wave schedule; bit 7 = the hi/lo residual GEMMs (epi 3, N % 256 == 0, grids of
- * >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel;
- * bit 8 / bit 9 = the persistent four-wave / staged-residual kernel issues a K-tile's 16 operand
- * DMAs spread over its B2 and B3 phases (10 + 6) instead of all in B2; bits 10 / 11 = a 12 + 4 /
- * 8 + 8 split on the persistent kernel; bit 12 = the 10 + 6 split with B3's DMAs in the gaps
- * without a fragment read.
+ * that schedule; off: those GEMMs run on SCHED 1); bit 4 = one tile per four-wave workgroup; bit 5 =
+ * split-K tail on the four-wave schedule; bit 7 = the hi/lo residual GEMMs (epi 3, N % 256 == 0, grids
+ * of >= 2 tiles per CU, default policy) on the staged-residual four-wave kernel;
+ * bits 8 / 9 (a K-tile's operand DMAs spread over B2 and B3) are always on since
+ * round 6; bit 13 = the caller's small one-tile grids (text tower) on the four-wave kernels.
  * Returns the previous bits. */
 int ce_set_gemm_variant(int bits);
-/* Attention-forward variant for A/B, bits: 1|2 = softmax mode (0 = every key
- * tile on the general online-softmax path: row max, offset accumulators, deferred rescale; 1 =
- * fixed-offset tiles once tile 0's row maxima lie within +-64 log2 units: no row max, no offset,
- * overflow-checked row sums, an overflowing tile redone on the general path; 2 = as 1 with the row
- * sums taken by the MFMA), 4 = one barrier per key tile, 8 = 16-B output stores, 16 = V^T fragments
- * read by inline asm (no vmcnt wait on the next tile's K/V DMA before P.V), 32 = tile 0 on the fixed
- * offset too (row sums checked from both sides), 64 = K/V DMAs through row-clipped buffer descriptors.
- * 128 = three K/V LDS slots (the next-but-one tile's DMA in flight; A/B only, measured slower: 3 workgroups
- * per CU instead of 4), 256 = key 0 folded into O / l before the key tiles, which then cover keys 1..L-1
- * (non-causal L with (L - 1) % 64 == 0: L = 577 runs 9 full tiles, no single-key masked tile; other L
- * drop the bit).  Selectable: 0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 253, 381; anything else restores the
- * default (381 = 125 + 256).  Causal launches (text tower) use mode 0 with bits 8, 16 and 64 when set.
- * Round-5 measurement variants of the non-causal (L - 1) % 64 == 0 launch (other
- * launches run 381 / 125): 2429 = 381 with tile 0's DMA and every prologue load issued at entry; 893 =
- * a persistent grid (3 workgroups per CU walking the q-blocks in rounds, the next block's Q / key-0 rows /
- * tile 0 DMA'd during the current block); 9085 = 893 with a per-block rotating s_setprio; 1405 / 1917 /
- * 10109 = 381 / 893 / 9085 recording timelines through ce_set_attn_trace.  All measured slower than 381.
+/* Attention-forward variant for A/B: 381 (default) = fixed-offset key tiles
+ * (once tile 0's row maxima lie within +-64 log2 units: no row max, no offset, overflow-checked row
+ * sums, an overflowing tile redone on the general online-softmax path), one barrier per key tile,
+ * 16-B output stores, V^T fragments by inline-asm ds_read_b64_tr_b16, K/V DMAs through row-clipped
+ * buffer descriptors, and key 0 folded into O / l before the key tiles, which then cover keys 1..L-1
+ * (non-causal L with (L - 1) % 64 == 0: L = 577 runs 9 full tiles, no single-key masked tile); 125 =
+ * the same without key 0 first (also what 381 runs for other L).  Anything else selects 381.  Causal
+ * launches (text tower) run the general-path kernel with the same loads and stores (88).  (The other
+ * variants of rounds 1-5 were measured slower and removed in round 6)
  * Returns the previous variant. */
 int ce_set_attn_variant(int var);
 /* Attention-backward kernel of the text-tower training for A/B (env CE_ATTN_BWD at first use): 3 = the
@@ -358,9 +351,9 @@ int ce_set_train_act_bwd_fuse(int on);
  * previous setting.  For A/B and parity tests. */
 int ce_set_fgemm_variant(int v);
 /* Launch counters per GEMM kernel path since the last reset: counts[path + epi] with path 0 =
- * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 = other
- * schedules, 10 = two-workgroup 256 x 128 (SCHED 12), and epi 0 = plain, 1 = LN statistics, 2 = LN
- * fold.  n <= 13 entries are written. */
+ * four-wave persistent (SCHED 11), 3 = 4-phase (SCHED 1), 6 = split-K tail fixup, 9 / 10 = unused
+ * since round 6 (removed schedules), and epi 0 = plain, 1 = LN statistics, 2 = LN fold.  n <= 13
+ * entries are written. */
 int ce_gemm_path_counts(int64_t* counts, int n, int reset);
 /* GEMM with an LN-fold / LN-stats epilogue (the folded ResidualAttentionBlock,
  * transformer.py:257-268), as the engine launches it:
@@ -375,17 +368,11 @@ int ce_gemm_path_counts(int64_t* counts, int n, int reset);
 int ce_kernel_gemm_bf16_epi(void* stream, const void* A, const void* W, int M, int N, int K, const float* bias,
                             int act, const float* resid, void* out, int out_dtype, int epi, void* xb,
                             void* stats_part, const void* fold_stats, const float* fold_c);
-/* Diagnostics: when buf (device, n_blocks x 4 uint64) is non-null, the SCHED 1 / SCHED 12 GEMM
- * kernels record per workgroup {s_memrealtime at start, after the K-loop, after wave 0's epilogue,
+/* Diagnostics: when buf (device, n_blocks x 4 uint64) is non-null, the GEMM kernels record per workgroup {s_memrealtime at start, after the K-loop, after wave 0's epilogue,
  * (XCC id << 32) | HW_ID} for blocks < n_blocks.  Null turns it off.  The pointer is process-wide
  * and every later GEMM launch of every handle and stream writes through it: diagnostics only, one
  * stream at a time, and call ce_set_gemm_trace(NULL, 0) (after a sync) before freeing buf. */
 int ce_set_gemm_trace(void* buf, int64_t n_blocks);
-/* Diagnostics: attention variant 1405 (= 381 with a timeline; ce_set_attn_variant) records per wave
- * {s_memrealtime at entry, after the prologue (Q, key 0), after tile 0's wait, after the key-tile
- * loop, after the output stores, (XCC id << 32) | HW_ID, -, -} into buf (device, n_waves x 8 uint64;
- * record = block * 4 + wave) for records < n_waves.  Same process-wide contract as ce_set_gemm_trace. */
-int ce_set_attn_trace(void* buf, int64_t n_waves);
 /* (mu, rstd) per row (eps 1e-5) from nslab 64-column slab statistics of an LN-stats GEMM:
  * stats [rows] float2, part [rows][nslab] float2. */
 int ce_kernel_ln_stats_finalize(void* stream, void* stats, const void* part, int rows, int nslab);

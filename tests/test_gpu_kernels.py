@@ -43,7 +43,7 @@ def gemm_ref(A, W, bias, act, resid):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 1024), (4617, 3072, 1024), (1154, 1024, 4096),
                                    (231, 2304, 768), (5, 768, 1024), (700, 832, 640), (1, 64, 64)])
 @pytest.mark.parametrize("variant", ["bias_bf16", "gelu_bf16", "qgelu_bf16", "resid_f32", "plain_f32"])
-@pytest.mark.parametrize("sched", [1, 2, 0, 6, 9, 10, 11, 12])
+@pytest.mark.parametrize("sched", [1, 11])
 def test_gemm(M, N, K, variant, sched):
     prev = _lib.lib().ce_set_gemm_schedule(sched)
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
@@ -100,10 +100,12 @@ def test_gemm_splitk_tail(M, N, K, variant):
 
 @pytest.mark.parametrize("M,N,K", [(33280, 1024, 1024), (20000, 3072, 1024), (17000, 1024, 4096)])
 @pytest.mark.parametrize("variant", ["gelu_bf16", "resid_f32", "bias_bf16"])
-@pytest.mark.parametrize("bits", [0, 1, 3, 35, 259, 291, 1283, 2307, 4355])
+@pytest.mark.parametrize("bits", [0, 1, 3, 19, 35])
 def test_gemm_persistent_multitile(M, N, K, variant, bits):
     """The four-wave persistent schedule (SCHED 11) with several tiles per workgroup, so the
-    epilogue -> next-tile hand-over (and its variant bits) runs; vs the f32 reference."""
+    epilogue -> next-tile hand-over (and its variant bits: 1 no drain, 2 the four-wave epilogues,
+    16 one tile per workgroup, 32 split-K tail) runs; vs the f32 reference.  The f32 residual
+    epilogue (and every GEMM with bit 1 off) takes SCHED 1."""
     L = _lib.lib()
     prev, prev_v = L.ce_set_gemm_schedule(11), L.ce_set_gemm_variant(bits)
     try:
@@ -129,12 +131,11 @@ def test_gemm_persistent_multitile(M, N, K, variant, bits):
 
 @pytest.mark.parametrize("M,N,act", [(20000, 3072, 0), (20000, 4096, 1), (20000, 4096, 2), (300, 1024, 1),
                                      (5602, 3072, 0), (4252, 4096, 1)])
-@pytest.mark.parametrize("bits", [1, 3, 35, 259, 291, 1283, 2307, 4355])
+@pytest.mark.parametrize("bits", [1, 3, 19, 35])
 def test_gemm_persistent_ln_fold(M, N, act, bits):
-    """SCHED 11 with the LN-fold epilogue (QKV / c_fc of the folded image tower), both epilogue
-    versions (bit 1: operands staged in LDS by DMA, buffer stores clipped at row M) and the split-K
-    tail (bit 5; 5602 x 3072 = 256 + 8 tiles, 4252 x 4096 = 256 + 16 tiles) and the operand DMAs
-    spread over B2 and B3 (bit 8):
+    """SCHED 11 with the LN-fold epilogue (QKV / c_fc of the folded image tower; bit 1 off: SCHED 1),
+    one tile per workgroup (bit 4) and the split-K tail (bit 5; 5602 x 3072 = 256 + 8 tiles,
+    4252 x 4096 = 256 + 16 tiles):
     out = act(rstd_m (A W^T - mu_m c_n) + d_n) vs torch f32; M % 256 != 0 exercises the row clip."""
     K = 1024
     L = _lib.lib()
@@ -166,10 +167,10 @@ def test_gemm_persistent_ln_fold(M, N, act, bits):
 
 
 @pytest.mark.parametrize("M,K", [(20000, 1024), (9000, 4096), (300, 1024)])
-@pytest.mark.parametrize("bits", [1, 3, 259])
+@pytest.mark.parametrize("bits", [1, 3, 19])
 def test_gemm_persistent_ln_stats(M, K, bits):
-    """SCHED 11 with the LN-statistics epilogue (out-proj / c_proj of the folded image tower), both
-    epilogue versions: out f32 = A W^T + bias + resid, xb = bf16(out), per-64-column (mean, M2)
+    """SCHED 11 with the LN-statistics epilogue (the f32-stream out-proj / c_proj; bit 1 off: SCHED 1),
+    one tile per workgroup (bit 4): out f32 = A W^T + bias + resid, xb = bf16(out), per-64-column (mean, M2)
     slab statistics, vs torch f32; rows >= M of every output stay untouched."""
     N = 1024
     L = _lib.lib()
@@ -204,17 +205,14 @@ def test_gemm_persistent_ln_stats(M, K, bits):
 
 @pytest.mark.parametrize("M,K,N,rhl", [(147712, 1024, 1024, 0), (147712, 4096, 1024, 0), (300, 1024, 1024, 0),
                                        (5000, 1024, 1024, 0), (147712, 1024, 1024, 1), (147712, 4096, 1024, 1),
-                                       (140001, 1024, 1024, 1), (131072, 192, 768, 1), (70000, 128, 1536, 1),
-                                       (147712, 1024, 1024, 2), (147712, 4096, 1024, 2), (140001, 1024, 1024, 2),
-                                       (131072, 192, 768, 2), (70000, 128, 1536, 2)])
+                                       (140001, 1024, 1024, 1), (131072, 192, 768, 1), (70000, 128, 1536, 1)])
 def test_gemm_ln_stats_hl(M, K, N, rhl):
     """The hi/lo residual-stream epilogues (SCHED 1, split-K tail at the bench shapes M = 256 * 577;
     rhl: epi 3 on the staged-residual four-wave kernel, variant bit 128, incl. a ragged last row
     tile, K = 2 and 3 K-tiles and N = 768 / 1536): epi 3 reads resid = hi + lo and writes
     v = A W^T + b + resid as planes hi = bf16(v), lo = bf16(v - hi) plus the slab statistics; epi 4
     writes v in f32.  vs torch f32: hi is the round-to-nearest bf16 of v, hi + lo within 2^-16 |v| of
-    v (f32 accumulation order aside).  rhl 2: the staged-residual kernel with its operand DMAs
-    spread over B2 and B3 (variant bit 512)."""
+    v (f32 accumulation order aside)."""
     L = _lib.lib()
     g = torch.Generator(device="cpu").manual_seed(M + K)
     A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
@@ -229,7 +227,7 @@ def test_gemm_ln_stats_hl(M, K, N, rhl):
     outp = torch.full((2, M, N), 7.0, device=DEV, dtype=torch.bfloat16)
     part = torch.full((M, ns, 2), 7.0, device=DEV)
     prev_v = L.ce_set_gemm_variant(-1)
-    L.ce_set_gemm_variant((prev_v & ~(128 | 512)) | (128 if rhl else 0) | (512 if rhl == 2 else 0))
+    L.ce_set_gemm_variant((prev_v & ~128) | (128 if rhl else 0))
     try:
         path_counts()
         _lib.call("ce_kernel_gemm_bf16_epi", S(), P(A), P(W), M, N, K, P(bias), 0, P(planes), None, _lib.CE_F32,
@@ -287,9 +285,10 @@ def attn_ref(qkv, B, L, H, causal):
     return (p @ v).permute(0, 2, 1, 3).reshape(B * L, D)
 
 
-@pytest.fixture(params=[0, 1, 2, 5, 9, 13, 16, 29, 61, 125, 381, 893, 1405, 2429, 9085], ids=lambda v: f"attn_var{v}")
+@pytest.fixture(params=[125, 381], ids=lambda v: f"attn_var{v}")
 def attn_var(request):
-    """Every attention forward variant (ce_set_attn_variant) against torch f32."""
+    """Both attention forward variants (ce_set_attn_variant) against torch f32 (causal
+    launches run the general-path kernel under either)."""
     prev = _lib.lib().ce_set_attn_variant(request.param)
     yield request.param
     _lib.lib().ce_set_attn_variant(prev)
@@ -360,7 +359,7 @@ def test_attention_wide_scores(scale, attn_var):
     ref = attn_ref(qkv, B, L, H, False)
     err = (out.float() - ref).abs().max().item()
     assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
-    prev = _lib.lib().ce_set_attn_variant(0)
+    prev = _lib.lib().ce_set_attn_variant(125 if attn_var == 381 else 381)
     try:
         base = run_attn(qkv, B, L, H, False)
     finally:

@@ -2,7 +2,7 @@
 (LN fold on QKV / c_fc, LN stats on out-proj / c_proj), schedules interleaved in one process
 (guide §5.4 rule 24), random data.
 
-    python tools/bench_gemm_epi.py --scheds 1,12 [--rounds 3] [--reps 10] [--only fc,qkv]
+    python tools/bench_gemm_epi.py --scheds 1,11 [--rounds 3] [--reps 10] [--only fc,qkv]
     (':' also separates schedule tokens: tools/gpu_run.sh turns ',' into spaces)
 A schedule token: <sched>[g<groupm>][a<auto>][s<stagger>][v<variant bits>][n]  (n: split-K tail off; a0: auto policy off;\ns<k>: first-round stagger of k x s_sleep 127 for half the CUs).
 """
@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--scheds", default="1,12")
+    ap.add_argument("--scheds", default="1,11")
     ap.add_argument("--only", default="")
     ap.add_argument("--warm-s", type=float, default=2.0)
     args = ap.parse_args()

@@ -26,7 +26,7 @@ SHAPES = {"qkv": (3072, 1024, 0, 2, False, True), "out": (1024, 1024, 0, 1, True
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="out")
-    ap.add_argument("--scheds", default="1,12")
+    ap.add_argument("--scheds", default="1,11")
     ap.add_argument("--batch", type=int, default=256)
     args = ap.parse_args()
     M = args.batch * 577

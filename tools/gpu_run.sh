@@ -11,6 +11,7 @@
 #   pmcs:<c1+c2+...>,<bench.py args>       one --pmc pass with several counters (within one pass's limits)
 #   py:<script>,<args>                     any python script (kernel A/B: tools/bench_gemm_epi.py,
 #                                          tools/bench_kernels.py; timelines: tools/gemm_trace.py)
+#   envpy:<VAR=VAL>,<script>,<args>        the same with one environment setting (e.g. CLIPEMBED_LIB=...)
 # Every step has its own time limit; the chain stops at the first failure.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -43,6 +44,8 @@ for step in "$@"; do
                -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-timing $rest \
                > gpurun_out/${TAG}_pmcs${n}.log 2>&1 ;;
     py)      timeout -k 10 600 python -u $args > gpurun_out/${TAG}_py$n.log 2>&1 ;;
+    envpy)   ev=${args%% *}; rest=${args#* }
+             timeout -k 10 600 env $ev python -u $rest > gpurun_out/${TAG}_py$n.log 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
