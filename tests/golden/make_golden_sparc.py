@@ -10,6 +10,7 @@ outputs only: selected token / patch rows of forward(), both scoring() modes and
     python tests/golden/make_golden_sparc.py        ->  tests/golden/sparc_full.npz
     python tests/golden/make_golden_sparc.py fulldepth   ->  tests/golden/sparc_fulldepth.npz (24 + 12 blocks)
     python tests/golden/make_golden_sparc.py dist   ->  tests/golden/sparc_dist.npz
+    python tests/golden/make_golden_sparc.py train  ->  tests/golden/sparc_train.npz
 
 `dist`: the reference SparcLoss(0.1) (train_sparc.py:105) and PACL ClipLoss(0.1) (train_pacl.py:106)
 on the CONCATENATION of two ranks' shards (tests/golden/dist_inputs.py), i.e. the value
@@ -111,8 +112,64 @@ def main_dist():
     print("wrote", path, out)
 
 
+# the SPARC head tensors train_sparc.py trains (its Adam sees every parameter, the frozen tower's have
+# no gradient); Patch_Projection's text_projection alias is the same module as linear_projection
+TRAIN_TENSORS = ["visual_projection.0.weight", "visual_projection.0.bias",
+                 "visual_projection.2.linear_projection.0.weight", "visual_projection.2.linear_projection.0.bias",
+                 "visual_projection.2.non_linear_projection.0.weight", "visual_projection.2.non_linear_projection.0.bias",
+                 "visual_projection.2.non_linear_projection.2.weight", "visual_projection.2.non_linear_projection.2.bias",
+                 "text_projection.0.weight", "text_projection.0.bias", "text_projection.2.weight", "text_projection.2.bias"]
+GRAD_ROWS = [0, 1, 383, 767]
+
+
+def main_train():
+    """One train_sparc.py step (train_sparc.py:29-37,91,106): sparc_rope(sigma = 1/576) forward, SparcLoss(0.1),
+    loss.backward(), torch.optim.Adam(lr = 1e-4).step(), on 3 images + 3 captions with 1-block towers (the
+    head math is depth-independent).  Dropout off (the module in eval mode: train_sparc.py's model.train()
+    draws torch RNG masks, which no other generator reproduces; the engine's dropout is tested against
+    the oracle with its own masks).  Writes the loss, every head gradient (1-d tensors whole, 2-d tensors'
+    norms and rows GRAD_ROWS) and the first Adam update of the same entries."""
+    import torch
+    from clipembed import weights as W
+    from clipembed.config import get_model_config
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    model_mod, _, pacl_mod = MG.import_reference()
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    clip, _ = MG.build_clip(model_mod, cfg)
+    heads = W.synthetic_pacl_heads(cfg.with_pacl(768))
+    imgs = torch.from_numpy(W.synthetic_images(3, seed=1400))
+    caps = W.synthetic_captions(3, seed=2400)
+    caps[1] = W.synthetic_captions(1, seed=2401, min_len=7, max_len=7)[0]
+    caps[2] = W.synthetic_captions(1, seed=2402, min_len=60, max_len=60)[0]
+    caps = torch.from_numpy(caps)
+    mod = build_sparc(pacl_mod, clip, pacl_mod.sparc_rope, heads, 1.0 / 576)
+    params = dict(mod.named_parameters())
+    opt = torch.optim.Adam(mod.parameters(), lr=1e-4)
+    opt.zero_grad()
+    v, l, g, mask = mod(imgs, caps)
+    loss = pacl_mod.SparcLoss(temperature=0.1)(v, l, g, mask)
+    loss.backward()
+    out = {"captions": caps.numpy(), "images_sha": np.array(MG.sha(imgs.numpy())), "loss": np.float32(loss.item()),
+           "v_sum": v.detach().numpy().sum((1, 2)), "g_sum": g.detach().numpy().sum((1, 2)), "mask": mask.numpy()}
+    before = {n: params[n].detach().clone() for n in TRAIN_TENSORS}
+    for n in TRAIN_TENSORS:
+        gr = params[n].grad.numpy()
+        out[f"grad_norm/{n}"] = np.float32(np.linalg.norm(gr.astype(np.float64)))
+        out[f"grad/{n}"] = gr if gr.ndim == 1 else np.ascontiguousarray(gr[GRAD_ROWS])
+    opt.step()
+    for n in TRAIN_TENSORS:
+        d = (params[n].detach() - before[n]).numpy()
+        out[f"update/{n}"] = d if d.ndim == 1 else np.ascontiguousarray(d[GRAD_ROWS])
+    path = os.path.join(HERE, "sparc_train.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, "loss", out["loss"], {k: v.shape for k, v in out.items() if k.startswith("grad/")})
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["dist"]:
         main_dist()
+    elif sys.argv[1:] == ["train"]:
+        main_train()
     else:
         main(full_depth=sys.argv[1:] == ["fulldepth"])

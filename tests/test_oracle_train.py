@@ -33,3 +33,32 @@ def test_text_train_restatement_matches_reference(golden):
         scale = np.abs(ref).max() + 1e-30
         assert np.abs(ours - ref).max() <= 1e-4 * scale, n
         np.testing.assert_allclose(float(gv.double().norm()), float(g[f"gnorm:{n}"]), rtol=1e-4, err_msg=n)
+
+
+def test_sparc_train_restatement_matches_reference(golden):
+    """Pins oracle/sparc_train_torch.py (the f32 autograd restatement of the SPARC head step the GPU tests
+    compare the engine against at larger batches) to the reference's own train_sparc.py step
+    (tests/golden/sparc_train.npz, make_golden_sparc.py train: sparc_rope(1/576) on 1-block towers,
+    SparcLoss(0.1), loss.backward(), dropout off): loss and every head gradient."""
+    import hashlib
+    from oracle.sparc_train_torch import HEAD_TENSORS, SparcTokens, TorchSparcTrainStep, rope_tokens
+    g = golden("sparc_train")
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    imgs = W.synthetic_images(3, seed=1400)
+    assert hashlib.sha256(np.ascontiguousarray(imgs).tobytes()).hexdigest() == str(g["images_sha"])
+    tok = SparcTokens(W.synthetic_state_dict(cfg), cfg)
+    caps = g["captions"]
+    pv = rope_tokens(tok.image_tokens(torch.from_numpy(imgs)))
+    tt = tok.text_tokens(torch.from_numpy(caps))
+    mask = (np.arange(caps.shape[1])[None, :] <= caps.argmax(-1)[:, None]).astype(np.float32)
+    np.testing.assert_array_equal(mask, g["mask"])
+    step = TorchSparcTrainStep(W.synthetic_pacl_heads(cfg.with_pacl(768)))
+    loss, grads, _ = step.loss_and_grads(pv, mask, text_tokens=tt)
+    np.testing.assert_allclose(loss, g["loss"], rtol=1e-5)
+    rows = [0, 1, 383, 767]
+    for n in HEAD_TENSORS:
+        gv = grads[n].numpy()
+        ref = g[f"grad/{n}"]
+        ours = gv if gv.ndim == 1 else gv[rows]
+        assert np.abs(ours - ref).max() <= 1e-4 * (np.abs(ref).max() + 1e-30), n
+        np.testing.assert_allclose(np.linalg.norm(gv.astype(np.float64)), g[f"grad_norm/{n}"], rtol=1e-4, err_msg=n)
