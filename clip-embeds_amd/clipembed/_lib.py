@@ -128,6 +128,13 @@ _SIGNATURES = {
                                     c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "ce_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                          c_float, c_float, c_int]),
+    "ce_sparc_train_bind": (c_int, [c_void_p, POINTER(Tensor), POINTER(Tensor), c_int]),
+    "ce_sparc_train_sync_weights": (c_int, [c_void_p, c_void_p]),
+    "ce_sparc_train_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                       c_float, c_float, ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
+    "ce_sparc_train_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float,
+                                         c_float, c_float, c_float, c_void_p]),
+    "ce_sparc_train_backward": (c_int, [c_void_p, c_void_p]),
     "ce_tokenizer_create": (c_int, [c_char_p, ctypes.c_size_t, POINTER(c_char_p), c_int, POINTER(c_void_p)]),
     "ce_tokenizer_destroy": (c_int, [c_void_p]),
     "ce_tokenizer_last_error": (c_char_p, []),

@@ -179,6 +179,14 @@ struct ce_handle {
     char* tr = nullptr;
     size_t tr_bytes = 0;
     int tr_B = 0;                // batch of the saved activations (0 = none)
+    // SPARC head training (ce_sparc_train_*): caller-owned f32 masters / gradient slots of the 12 head
+    // tensors, the saved activations of the last ce_sparc_train_forward and its settings
+    std::map<std::string, std::pair<float*, float*>> sp_bound;
+    char* sp = nullptr;
+    size_t sp_bytes = 0;
+    int sp_B = 0, sp_P = 0, sp_T = 0, sp_text = 0, sp_state = 0;   // state: 1 forward done, 2 loss grad done
+    float sp_sigma = 0.f, sp_drop = 0.f;
+    uint64_t sp_seed = 0;
     std::vector<KStat> stats;
     std::map<std::string, int> stat_idx;
     std::vector<Pending> pending;
@@ -1224,6 +1232,7 @@ int ce_destroy(ce_handle* h) {
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->pool) (void)hipFree(h->pool);
     if (h->tr) (void)hipFree(h->tr);
+    if (h->sp) (void)hipFree(h->sp);
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->prep_host) (void)hipHostFree(h->prep_host);
     if (h->prep_dev) (void)hipFree(h->prep_dev);
@@ -2065,6 +2074,359 @@ int ce_preprocess_images_boxes(ce_handle* h, void* stream, const uint8_t* images
                                void* out) {
     if (!boxes) return fail(CE_ERR_INVALID, "ce_preprocess_images_boxes: null boxes");
     return preprocess_impl(h, stream, images, offsets, heights, widths, boxes, B, CE_PRE_CLIP_BICUBIC, out_dtype, out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// SPARC head training (train_sparc.py:29-37,91,106; model/pacl.py:380-584).  Forward keeps the
+// activations in h->sp; loss_grad takes the global loss's gradient w.r.t. this rank's normalised
+// means and local-term inputs; backward runs it down to the 12 head tensors.
+namespace {
+
+const char* const kSparcHead[12] = {
+    "visual_projection.0.weight", "visual_projection.0.bias",
+    "visual_projection.2.linear_projection.0.weight", "visual_projection.2.linear_projection.0.bias",
+    "visual_projection.2.non_linear_projection.0.weight", "visual_projection.2.non_linear_projection.0.bias",
+    "visual_projection.2.non_linear_projection.2.weight", "visual_projection.2.non_linear_projection.2.bias",
+    "text_projection.0.weight", "text_projection.0.bias", "text_projection.2.weight", "text_projection.2.bias"};
+
+struct SparcWs {
+    int B, P, T, Dv, E, Pd;
+    long N1, Nt;
+    float *xv, *ylin, *v, *xt, *ht, *l, *Ln, *S, *Wt, *G, *Gn, *mv, *ml, *dgi, *dgt, *R, *dR, *dRT, *part;
+    float *dGn, *dLn, *dG, *dS, *tT, *dv, *dh, *dl, *dlT, *dht, *cs, *lng, *abw, *gpart;
+    float2 *stv, *stt;
+    bf16_t *hv, *a, *g, *dvb, *da, *W2T, *WlT, *W1T;
+};
+
+size_t sparc_layout(const ce_handle* h, int B, int P, int T, SparcWs* w, char* base) {
+    const ce_config& c = h->cfg;
+    SparcWs t{};
+    t.B = B; t.P = P; t.T = T; t.Dv = c.vision.width; t.E = c.embed_dim; t.Pd = c.pacl_dim;
+    t.N1 = (long)B * P; t.Nt = (long)B * T;
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* r = base ? base + off : nullptr;
+        off += align256(bytes);
+        return r;
+    };
+    const long N1 = t.N1, Nt = t.Nt, Dv = t.Dv, E = t.E, Pd = t.Pd;
+    const long BTP = (long)B * T * P, BTD = (long)B * T * Pd, BTT = (long)B * T * T;
+    t.xv = (float*)take(N1 * Dv * 4);   t.stv = (float2*)take(N1 * 8);   t.hv = (bf16_t*)take(N1 * Dv * 2);
+    t.a = (bf16_t*)take(N1 * Pd * 2);   t.g = (bf16_t*)take(N1 * Pd * 2);
+    t.ylin = (float*)take(N1 * Pd * 4); t.v = (float*)take(N1 * Pd * 4);
+    t.xt = (float*)take(Nt * E * 4);    t.stt = (float2*)take(Nt * 8);   t.ht = (float*)take(Nt * E * 4);
+    t.l = (float*)take(Nt * Pd * 4);    t.Ln = (float*)take(Nt * Pd * 4);
+    t.S = (float*)take(BTP * 4);        t.Wt = (float*)take(BTP * 4);
+    t.G = (float*)take(BTD * 4);        t.Gn = (float*)take(BTD * 4);
+    t.mv = (float*)take((long)B * Pd * 4); t.ml = (float*)take((long)B * Pd * 4);
+    t.dgi = (float*)take((long)B * Pd * 4); t.dgt = (float*)take((long)B * Pd * 4);
+    t.R = (float*)take(BTT * 4);        t.dR = (float*)take(BTT * 4);    t.dRT = (float*)take(BTT * 4);
+    t.part = (float*)take((long)B * 3 * 4 + 32);
+    t.dGn = (float*)take(BTD * 4);      t.dLn = (float*)take(BTD * 4);   t.dG = (float*)take(BTD * 4);
+    t.dS = (float*)take(BTP * 4);       t.tT = (float*)take(BTP * 4);
+    t.dv = (float*)take(N1 * Pd * 4);   t.dvb = (bf16_t*)take(N1 * Pd * 2); t.da = (bf16_t*)take(N1 * Pd * 2);
+    t.dh = (float*)take(N1 * Dv * 4);
+    t.dl = (float*)take(Nt * Pd * 4);   t.dlT = (float*)take(Nt * Pd * 4); t.dht = (float*)take(Nt * E * 4);
+    t.W2T = (bf16_t*)take(Pd * Pd * 2); t.WlT = (bf16_t*)take(Dv * Pd * 2); t.W1T = (bf16_t*)take(Dv * Pd * 2);
+    t.cs = (float*)take(std::max(ce::colsum_scratch_floats((int)N1, (int)Pd), ce::colsum_scratch_floats((int)Nt, (int)Pd)) * 4);
+    t.lng = (float*)take(std::max(ce::ln_grad_scratch_floats(N1, (int)Dv), ce::ln_grad_scratch_floats(Nt, (int)E)) * 4);
+    t.abw = (float*)take(std::max(ce::act_bwd_colsum_scratch_floats((int)N1, (int)Pd), ((N1 + 127) / 128) * Pd) * 4);
+    t.gpart = (float*)take(ce::kGemmPartElems * 4);
+    if (w) *w = t;
+    return off;
+}
+
+float* sp_param(ce_handle* h, const char* n) { return h->sp_bound.at(n).first; }
+float* sp_grad(ce_handle* h, const char* n) { return h->sp_bound.at(n).second; }
+
+int sparc_fgemm(ce_handle* h, hipStream_t s, const char* tag, const float* A, long lda, long sA, const float* B, long ldb,
+                long sB, float* C, long ldc, long sC, int M, int N, int K, int batch, float alpha, bool b_nk,
+                const float* bias = nullptr, bool accumulate = false) {
+    ce::FGemmParams f{};
+    f.A = A; f.lda = lda; f.sA = sA; f.B = B; f.ldb = ldb; f.sB = sB; f.C = C; f.ldc = ldc; f.sC = sC;
+    f.M = M; f.N = N; f.K = K; f.batch = batch; f.alpha = alpha; f.bias = bias; f.accumulate = accumulate ? 1 : 0;
+    return timed(h, s, tag, 2.0 * M * N * K * batch, 0.0, [&] { return ce::launch_fgemm(f, b_nk, s); });
+}
+
+}  // namespace
+
+int ce_sparc_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* grads, int n) {
+    if (!h || (n > 0 && (!params || !grads))) return fail(CE_ERR_INVALID, "ce_sparc_train_bind: null argument");
+    if (h->cfg.pacl_dim <= 0) return fail(CE_ERR_STATE, "ce_sparc_train_bind: handle has no PACL / SPARC head");
+    std::map<std::string, std::pair<float*, float*>> b;
+    for (int i = 0; i < n; ++i) {
+        if (!params[i].name || !grads[i].name || strcmp(params[i].name, grads[i].name) != 0)
+            return fail(CE_ERR_INVALID, "ce_sparc_train_bind: entry %d: params and grads must name the same tensor", i);
+        const std::string name = canonical(h, params[i].name);
+        if (std::find_if(std::begin(kSparcHead), std::end(kSparcHead), [&](const char* k) { return name == k; }) ==
+            std::end(kSparcHead))
+            return fail(CE_ERR_INVALID, "ce_sparc_train_bind: '%s' is not a SPARC head tensor", params[i].name);
+        const WSpec& sp = h->specs.at(name);
+        if (params[i].dtype != CE_F32 || grads[i].dtype != CE_F32 || !params[i].data || !grads[i].data)
+            return fail(CE_ERR_INVALID, "ce_sparc_train_bind: '%s' needs f32 device buffers", params[i].name);
+        for (const ce_tensor* t : {&params[i], &grads[i]}) {
+            bool ok = t->ndim == (int)sp.shape.size();
+            for (int d = 0; ok && d < t->ndim; ++d) ok = t->shape[d] == sp.shape[d];
+            if (!ok) return fail(CE_ERR_INVALID, "ce_sparc_train_bind: '%s' has the wrong shape", params[i].name);
+        }
+        b[name] = {(float*)params[i].data, (float*)grads[i].data};
+    }
+    for (const char* k : kSparcHead)
+        if (!b.count(k)) return fail(CE_ERR_INVALID, "ce_sparc_train_bind: head tensor '%s' not bound", k);
+    h->sp_bound = b;
+    h->sp_state = 0;
+    return CE_OK;
+}
+
+int ce_sparc_train_sync_weights(ce_handle* h, void* stream) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_sparc_train_sync_weights: null handle");
+    if (h->sp_bound.empty()) return fail(CE_ERR_STATE, "ce_sparc_train_sync_weights: no head bound (ce_sparc_train_bind)");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    for (auto& kv : h->sp_bound) {
+        const WSpec& sp = h->specs.at(kv.first);
+        const size_t n = spec_elems(h, kv.first);
+        void*& dp = h->dptr[kv.first];
+        if (!dp) {
+            if (hipMalloc(&dp, n * (sp.st == ST_BF16 ? 2 : 4)) != hipSuccess) {
+                (void)hipGetLastError();
+                h->dptr.erase(kv.first);
+                return fail(CE_ERR_OOM, "ce_sparc_train_sync_weights: cannot allocate '%s'", kv.first.c_str());
+            }
+        }
+        if (sp.st == ST_F32_T) {     // text_projection.2.weight [Pd][E] kept transposed for the f32 GEMM
+            CE_TRY(check_launch(ce::launch_transpose_add(kv.second.first, nullptr, (float*)dp, 1, (int)sp.shape[0],
+                                                         (int)sp.shape[1], s), "sparc weight sync"));
+        } else if (sp.st == ST_BF16 || sp.st == ST_F32) {
+            const long row = sp.shape.size() == 2 ? sp.shape[1] : 1;
+            CE_TRY(check_launch(ce::launch_weight_from_master(dp, sp.st == ST_BF16, kv.second.first, (long)n, row, 0, 1.f, s),
+                                "sparc weight sync"));
+        } else {
+            return fail(CE_ERR_INVALID, "ce_sparc_train_sync_weights: '%s' has an unsupported storage", kv.first.c_str());
+        }
+        h->loaded[kv.first] = true;
+    }
+    return CE_OK;
+}
+
+int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens, int B, int P, int rope,
+                           const float* text, int text_mode, int T, float sigma, float dropout, uint64_t seed,
+                           float* out_v, float* out_l, float* out_g) {
+    if (!h || !patch_tokens || !text) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: null argument");
+    if (h->sp_bound.empty()) return fail(CE_ERR_STATE, "ce_sparc_train_forward: no head bound (ce_sparc_train_bind)");
+    if (B <= 0 || P <= 0 || T <= 0 || T > 80) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: bad sizes (T <= 80)");
+    if (rope != CE_ROPE_NONE && rope != CE_ROPE_BEFORE) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: rope NONE / BEFORE");
+    if (rope == CE_ROPE_BEFORE && P != h->G * h->G)
+        return fail(CE_ERR_INVALID, "ce_sparc_train_forward: rope tables cover %d patches", h->G * h->G);
+    if (text_mode != 0 && text_mode != 1) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: text_mode 0 or 1");
+    if (!(dropout >= 0.f && dropout < 1.f)) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: dropout in [0, 1)");
+    CE_TRY(check_ready(h, true));
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    CE_TRY(grow_buffer(h->sp, h->sp_bytes, sparc_layout(h, B, P, T, nullptr, nullptr)));
+    SparcWs w;
+    sparc_layout(h, B, P, T, &w, h->sp);
+    const int Dv = w.Dv, E = w.E, Pd = w.Pd;
+    const int N1 = (int)w.N1;
+    h->sp_state = 0;
+    // ---- visual head: [apply_rope] -> LayerNorm -> Dropout -> Patch_Projection (pacl.py:35-48,480-484) ----
+    if (rope) CE_TRY(check_launch(ce::launch_rope(w.xv, patch_tokens, B, P, Dv, h->rc_v, h->rs_v, s), "sparc rope"));
+    else HIP_TRY(hipMemcpyAsync(w.xv, patch_tokens, (size_t)w.N1 * Dv * 4, hipMemcpyDeviceToDevice, s));
+    CE_TRY(timed(h, s, "sparc_ln_v", 0.0, 6.0 * w.N1 * Dv, [&] {
+        return ce::launch_ln_drop(w.xv, W(h, "visual_projection.0.weight"), W(h, "visual_projection.0.bias"), w.N1, Dv,
+                                  dropout, 2 * seed, w.hv, true, w.stv, s); }));
+    CE_TRY(tgemm(h, s, "sparc_head_v", w.hv, Dv, W<bf16_t>(h, "visual_projection.2.linear_projection.0.weight"), Dv, N1,
+                 Pd, Dv, W(h, "visual_projection.2.linear_projection.0.bias"), ce::ACT_NONE_, nullptr, w.ylin, false, w.gpart));
+    {
+        ce::GemmParams p{};     // GELU(Linear) with the pre-activation kept for the backward
+        p.A = w.hv; p.lda = Dv; p.W = W<bf16_t>(h, "visual_projection.2.non_linear_projection.0.weight"); p.ldw = Dv;
+        p.M = N1; p.N = Pd; p.K = Dv;
+        p.bias = W(h, "visual_projection.2.non_linear_projection.0.bias");
+        p.out = w.g; p.ldo = Pd; p.pre_out = w.a;
+        p.part = w.gpart; p.part_elems = ce::kGemmPartElems;
+        CE_TRY(timed(h, s, "sparc_head_v", 2.0 * N1 * Pd * Dv, 0.0, [&] { return ce::launch_gemm(p, ce::ACT_GELU_, true, s); }));
+    }
+    CE_TRY(tgemm(h, s, "sparc_head_v", w.g, Pd, W<bf16_t>(h, "visual_projection.2.non_linear_projection.2.weight"), Pd, N1,
+                 Pd, Pd, W(h, "visual_projection.2.non_linear_projection.2.bias"), ce::ACT_NONE_, w.ylin, w.v, false, w.gpart));
+    // ---- text: text_projection = LayerNorm -> Dropout -> Linear (pacl.py:431-436), or the embeddings ----
+    if (text_mode == 0) {
+        HIP_TRY(hipMemcpyAsync(w.xt, text, (size_t)w.Nt * E * 4, hipMemcpyDeviceToDevice, s));
+        CE_TRY(timed(h, s, "sparc_ln_t", 0.0, 8.0 * w.Nt * E, [&] {
+            return ce::launch_ln_drop(w.xt, W(h, "text_projection.0.weight"), W(h, "text_projection.0.bias"), w.Nt, E,
+                                      dropout, 2 * seed + 1, w.ht, false, w.stt, s); }));
+        CE_TRY(sparc_fgemm(h, s, "sparc_head_t", w.ht, E, 0, sp_param(h, "text_projection.2.weight"), E, 0, w.l, Pd, 0,
+                           (int)w.Nt, Pd, E, 1, 1.f, true, W(h, "text_projection.2.bias")));
+    } else {
+        HIP_TRY(hipMemcpyAsync(w.l, text, (size_t)w.Nt * Pd * 4, hipMemcpyDeviceToDevice, s));
+    }
+    CE_TRY(check_launch(ce::launch_l2norm(w.Ln, w.l, (int)w.Nt, Pd, s), "sparc normalize"));
+    // ---- alignment (pacl.py:455-476) ----
+    CE_TRY(sparc_fgemm(h, s, "sparc_sim", w.l, Pd, (long)T * Pd, w.v, Pd, (long)P * Pd, w.S, P, (long)T * P, T, P, Pd, B,
+                       1.f, true));
+    HIP_TRY(hipMemcpyAsync(w.Wt, w.S, (size_t)B * T * P * 4, hipMemcpyDeviceToDevice, s));
+    CE_TRY(check_launch(ce::launch_sparc_weights(w.Wt, (long)B * T, P, sigma, s), "sparc weights"));
+    CE_TRY(sparc_fgemm(h, s, "sparc_group", w.Wt, P, (long)T * P, w.v, Pd, (long)P * Pd, w.G, Pd, (long)T * Pd, T, Pd, P,
+                       B, 1.f, false));
+    CE_TRY(check_launch(ce::launch_l2norm(w.Gn, w.G, B * T, Pd, s), "sparc normalize"));
+    if (out_v) HIP_TRY(hipMemcpyAsync(out_v, w.v, (size_t)w.N1 * Pd * 4, hipMemcpyDeviceToDevice, s));
+    if (out_l) HIP_TRY(hipMemcpyAsync(out_l, w.Ln, (size_t)w.Nt * Pd * 4, hipMemcpyDeviceToDevice, s));
+    if (out_g) HIP_TRY(hipMemcpyAsync(out_g, w.Gn, (size_t)B * T * Pd * 4, hipMemcpyDeviceToDevice, s));
+    h->sp_B = B; h->sp_P = P; h->sp_T = T; h->sp_text = text_mode;
+    h->sp_sigma = sigma; h->sp_drop = dropout; h->sp_seed = seed;
+    h->sp_state = 1;
+    return CE_OK;
+}
+
+int ce_sparc_train_loss_grad(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg, int row0,
+                             const float* mask, float mask_total, float temperature, float global_weight,
+                             float local_weight, float* parts) {
+    if (!h || !img_all || !txt_all || !mask || !parts) return fail(CE_ERR_INVALID, "ce_sparc_train_loss_grad: null argument");
+    if (h->sp_state < 1) return fail(CE_ERR_STATE, "ce_sparc_train_loss_grad: no ce_sparc_train_forward before it");
+    const int B = h->sp_B, T = h->sp_T;
+    CE_TRY(check_shard("ce_sparc_train_loss_grad", Bg, row0, B, h->cfg.pacl_dim));
+    if (!(temperature > 0.f) || !(mask_total > 0.f)) return fail(CE_ERR_INVALID, "ce_sparc_train_loss_grad: temperature / mask_total");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    SparcWs w;
+    sparc_layout(h, B, h->sp_P, T, &w, h->sp);
+    const int Pd = w.Pd;
+    const float scale = 1.0f / temperature;
+    // local term (pacl.py:522-556,575-580): R = scale Gn Ln^T, dR, dGn = scale dR Ln, dLn = scale dR^T Gn
+    CE_TRY(sparc_fgemm(h, s, "sparc_loss_local", w.Gn, Pd, (long)T * Pd, w.Ln, Pd, (long)T * Pd, w.R, T, (long)T * T, T, T,
+                       Pd, B, scale, true));
+    CE_TRY(check_launch(ce::launch_local_grad(w.R, mask, B, T, local_weight * 0.5f / mask_total, w.dR, w.dRT, w.part, s),
+                        "sparc local grad"));
+    CE_TRY(sparc_fgemm(h, s, "sparc_loss_local", w.dR, T, (long)T * T, w.Ln, Pd, (long)T * Pd, w.dGn, Pd, (long)T * Pd, T, Pd,
+                       T, B, scale, false));
+    CE_TRY(sparc_fgemm(h, s, "sparc_loss_local", w.dRT, T, (long)T * T, w.Gn, Pd, (long)T * Pd, w.dLn, Pd, (long)T * Pd, T,
+                       Pd, T, B, scale, false));
+    // global term (pacl.py:563-570) over the whole gathered batch (every rank computes the Bg x Bg
+    // softmaxes; its rows of the gradient are this rank's): M = dLi + dLt^T
+    const size_t nL = (size_t)Bg * Bg;
+    CE_TRY(ensure_tmp(h, (6 * nL + 2 * (size_t)Bg) * 4));
+    float* Li = (float*)h->tmp;
+    float* Lt = Li + nL;
+    float* dLi = Lt + nL;
+    float* dLt = dLi + nL;
+    float* M = dLt + nL;
+    float* MT = M + nL;
+    float* lr = MT + nL;
+    float* lc = lr + Bg;
+    {
+        ce::FGemmParams a{};
+        a.A = img_all; a.lda = Pd; a.B = txt_all; a.ldb = Pd; a.C = Li; a.ldc = Bg; a.Ct = Lt; a.ldct = Bg;
+        a.M = Bg; a.N = Bg; a.K = Pd; a.batch = 1; a.alpha = scale;
+        CE_TRY(check_launch(ce::launch_fgemm(a, true, s), "sparc global logits"));
+    }
+    const float wg = global_weight * 0.5f / (float)Bg;
+    CE_TRY(check_launch(ce::launch_ce_diag_grad(Li, Bg, Bg, wg, dLi, lr, s), "sparc global grad"));
+    CE_TRY(check_launch(ce::launch_ce_diag_grad(Lt, Bg, Bg, wg, dLt, lc, s), "sparc global grad"));
+    CE_TRY(check_launch(ce::launch_transpose_add(dLt, dLi, M, 1, Bg, Bg, s), "sparc global grad"));
+    CE_TRY(check_launch(ce::launch_transpose_add(dLi, dLt, MT, 1, Bg, Bg, s), "sparc global grad"));
+    CE_TRY(sparc_fgemm(h, s, "sparc_loss_global", M + (size_t)row0 * Bg, Bg, 0, txt_all, Pd, 0, w.dgi, Pd, 0, B, Pd, Bg, 1,
+                       scale, false));
+    CE_TRY(sparc_fgemm(h, s, "sparc_loss_global", MT + (size_t)row0 * Bg, Bg, 0, img_all, Pd, 0, w.dgt, Pd, 0, B, Pd, Bg, 1,
+                       scale, false));
+    CE_TRY(check_launch(ce::launch_loss_parts(parts, lr + row0, lc + row0, B, w.part, B, s), "sparc loss parts"));
+    h->sp_state = 2;
+    return CE_OK;
+}
+
+int ce_sparc_train_backward(ce_handle* h, void* stream) {
+    if (!h) return fail(CE_ERR_INVALID, "ce_sparc_train_backward: null handle");
+    if (h->sp_state < 2) return fail(CE_ERR_STATE, "ce_sparc_train_backward: needs ce_sparc_train_forward + _loss_grad first");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int B = h->sp_B, P = h->sp_P, T = h->sp_T;
+    SparcWs w;
+    sparc_layout(h, B, P, T, &w, h->sp);
+    const int Dv = w.Dv, E = w.E, Pd = w.Pd, N1 = (int)w.N1, Nt = (int)w.Nt;
+    const float p = h->sp_drop;
+    const uint64_t seed = h->sp_seed;
+    // ---- means + normalise (pacl.py:566-567) ----
+    CE_TRY(check_launch(ce::launch_mean_mid(w.mv, w.v, B, P, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_mean_mid(w.ml, w.Ln, B, T, Pd, s), "sparc bwd"));
+    float* dmv = w.dR;          // (B x Pd <= B x T x T; dR / dRT are free after ce_sparc_train_loss_grad)
+    float* dml = w.dRT;
+    CE_TRY(check_launch(ce::launch_l2norm_bwd(dmv, w.mv, w.dgi, B, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_l2norm_bwd(dml, w.ml, w.dgt, B, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_bcast_add_mid(w.dLn, dml, B, T, Pd, 1.0f / T, s), "sparc bwd"));
+    // ---- alignment (pacl.py:455-476) ----
+    CE_TRY(check_launch(ce::launch_l2norm_bwd(w.dG, w.G, w.dGn, B * T, Pd, s), "sparc bwd"));
+    // dW = dG v^T; dv = W^T dG
+    CE_TRY(sparc_fgemm(h, s, "sparc_bwd_align", w.dG, Pd, (long)T * Pd, w.v, Pd, (long)P * Pd, w.dS, P, (long)T * P, T, P,
+                       Pd, B, 1.f, true));
+    CE_TRY(check_launch(ce::launch_transpose_add(w.Wt, nullptr, w.tT, B, T, P, s), "sparc bwd"));
+    CE_TRY(sparc_fgemm(h, s, "sparc_bwd_align", w.tT, T, (long)P * T, w.dG, Pd, (long)T * Pd, w.dv, Pd, (long)P * Pd, P, Pd,
+                       T, B, 1.f, false));
+    CE_TRY(check_launch(ce::launch_align_bwd(w.S, w.dS, (long)B * T, P, h->sp_sigma, s), "sparc align bwd"));
+    // dl = dS v; dv += dS^T l; dv += d mean_v / P
+    CE_TRY(sparc_fgemm(h, s, "sparc_bwd_align", w.dS, P, (long)T * P, w.v, Pd, (long)P * Pd, w.dl, Pd, (long)T * Pd, T, Pd,
+                       P, B, 1.f, false));
+    CE_TRY(check_launch(ce::launch_transpose_add(w.dS, nullptr, w.tT, B, T, P, s), "sparc bwd"));
+    CE_TRY(sparc_fgemm(h, s, "sparc_bwd_align", w.tT, T, (long)P * T, w.l, Pd, (long)T * Pd, w.dv, Pd, (long)P * Pd, P, Pd,
+                       T, B, 1.f, false, nullptr, true));
+    CE_TRY(check_launch(ce::launch_bcast_add_mid(w.dv, dmv, B, P, Pd, 1.0f / P, s), "sparc bwd"));
+    // dl += normalize backward of dLn
+    CE_TRY(check_launch(ce::launch_l2norm_bwd(w.dG, w.l, w.dLn, Nt, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_axpy(w.dl, w.dG, (long)Nt * Pd, 1.f, s), "sparc bwd"));
+    // ---- text head: Linear, Dropout, LayerNorm (f32) ----
+    if (h->sp_text == 0) {
+        CE_TRY(check_launch(ce::launch_colsum(sp_grad(h, "text_projection.2.bias"), w.dl, true, Pd, Nt, Pd, 1.f, false, w.cs, s),
+                            "sparc bwd"));
+        CE_TRY(check_launch(ce::launch_transpose_add(w.dl, nullptr, w.dlT, 1, Nt, Pd, s), "sparc bwd"));
+        CE_TRY(sparc_fgemm(h, s, "sparc_bwd_head_t", w.dlT, Nt, 0, w.ht, E, 0, sp_grad(h, "text_projection.2.weight"), E, 0,
+                           Pd, E, Nt, 1, 1.f, false));
+        CE_TRY(sparc_fgemm(h, s, "sparc_bwd_head_t", w.dl, Pd, 0, sp_param(h, "text_projection.2.weight"), E, 0, w.dht, E, 0,
+                           Nt, E, Pd, 1, 1.f, false));
+        CE_TRY(check_launch(ce::launch_ln_grad(w.dht, w.xt, w.stt, Nt, E, p, 2 * seed + 1, sp_grad(h, "text_projection.0.weight"),
+                                               sp_grad(h, "text_projection.0.bias"), w.lng, s), "sparc ln grad"));
+    } else {
+        for (const char* n : {"text_projection.0.weight", "text_projection.0.bias", "text_projection.2.weight",
+                              "text_projection.2.bias"})
+            HIP_TRY(hipMemsetAsync(sp_grad(h, n), 0, spec_elems(h, n) * 4, s));
+    }
+    // ---- visual head: Patch_Projection, Dropout, LayerNorm (bf16 GEMM operands, f32 accumulation) ----
+    CE_TRY(check_launch(ce::launch_cast_bf16(w.dvb, w.dv, (long)N1 * Pd, s), "sparc bwd"));
+    float* dbl = sp_grad(h, "visual_projection.2.linear_projection.0.bias");
+    CE_TRY(check_launch(ce::launch_colsum(dbl, w.dv, true, Pd, N1, Pd, 1.f, false, w.cs, s), "sparc bwd"));
+    HIP_TRY(hipMemcpyAsync(sp_grad(h, "visual_projection.2.non_linear_projection.2.bias"), dbl, (size_t)Pd * 4,
+                           hipMemcpyDeviceToDevice, s));
+    CE_TRY(tgemm_tn(h, s, "sparc_bwd_dw", w.dvb, Pd, w.g, Pd, Pd, Pd, N1,
+                    sp_grad(h, "visual_projection.2.non_linear_projection.2.weight"), w.gpart));
+    CE_TRY(tgemm_tn(h, s, "sparc_bwd_dw", w.dvb, Pd, w.hv, Dv, Pd, Dv, N1,
+                    sp_grad(h, "visual_projection.2.linear_projection.0.weight"), w.gpart));
+    CE_TRY(check_launch(ce::launch_transpose_bf16(w.W2T, Pd, W<bf16_t>(h, "visual_projection.2.non_linear_projection.2.weight"),
+                                                  false, Pd, Pd, Pd, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_transpose_bf16(w.WlT, Pd, W<bf16_t>(h, "visual_projection.2.linear_projection.0.weight"),
+                                                  false, Dv, Pd, Dv, Pd, s), "sparc bwd"));
+    CE_TRY(check_launch(ce::launch_transpose_bf16(w.W1T, Pd, W<bf16_t>(h, "visual_projection.2.non_linear_projection.0.weight"),
+                                                  false, Dv, Pd, Dv, Pd, s), "sparc bwd"));
+    // dA = GELU'(a) * (dv W2) and the GELU bias gradient, fused in the GEMM's epilogue where the four-wave
+    // kernel takes the shape (as the text-tower backward's c_fc, capi.hip run_text_backward)
+    float* db1 = sp_grad(h, "visual_projection.2.non_linear_projection.0.bias");
+    {
+        ce::GemmParams pb{};
+        pb.A = w.dvb; pb.lda = Pd; pb.W = w.W2T; pb.ldw = Pd;
+        pb.M = N1; pb.N = Pd; pb.K = Pd;
+        pb.out = w.da; pb.ldo = Pd;
+        pb.bwd_pre = w.a; pb.bwd_part = w.abw;
+        if (ce::gemm_act_bwd_fused(pb, ce::ACT_GELU_)) {
+            CE_TRY(timed(h, s, "sparc_bwd_dx", 2.0 * N1 * Pd * Pd, 0.0, [&] { return ce::launch_gemm_act_bwd(pb, ce::ACT_GELU_, s); }));
+            CE_TRY(check_launch(ce::launch_colsum_finish(db1, w.abw, (N1 + 127) / 128, Pd, s), "sparc bwd"));
+        } else {
+            CE_TRY(tgemm(h, s, "sparc_bwd_dx", w.dvb, Pd, w.W2T, Pd, N1, Pd, Pd, nullptr, 0, nullptr, w.da, true, w.gpart));
+            CE_TRY(check_launch(ce::launch_act_bwd_colsum(w.da, w.a, w.da, N1, Pd, ce::ACT_GELU_, db1, w.abw, s), "sparc bwd"));
+        }
+    }
+    CE_TRY(tgemm_tn(h, s, "sparc_bwd_dw", w.da, Pd, w.hv, Dv, Pd, Dv, N1,
+                    sp_grad(h, "visual_projection.2.non_linear_projection.0.weight"), w.gpart));
+    CE_TRY(tgemm(h, s, "sparc_bwd_dx", w.dvb, Pd, w.WlT, Pd, N1, Dv, Pd, nullptr, 0, nullptr, w.dh, false, w.gpart));
+    CE_TRY(tgemm(h, s, "sparc_bwd_dx", w.da, Pd, w.W1T, Pd, N1, Dv, Pd, nullptr, 0, w.dh, w.dh, false, w.gpart));
+    CE_TRY(check_launch(ce::launch_ln_grad(w.dh, w.xv, w.stv, N1, Dv, p, 2 * seed, sp_grad(h, "visual_projection.0.weight"),
+                                           sp_grad(h, "visual_projection.0.bias"), w.lng, s), "sparc ln grad"));
+    h->sp_state = 1;    // (a new loss_grad is needed before another backward)
+    return CE_OK;
 }
 
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out) {

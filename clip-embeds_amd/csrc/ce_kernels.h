@@ -196,6 +196,7 @@ struct FGemmParams {
     float alpha;
     const float* bias;     // nullable [N]
     float* Ct; long ldct;  // nullable: also write C^T (batch 1 only)
+    int accumulate = 0;    // C += alpha A B' (+ bias) instead of C = ...
 };
 hipError_t launch_fgemm(const FGemmParams& p, bool b_nk, hipStream_t s);
 // rows of D: x / max(||x||, 1e-12)
@@ -214,6 +215,27 @@ hipError_t launch_sparc_weights(float* sim, long rows, int P, float sigma, hipSt
 hipError_t launch_rope(float* out, const float* x, int B, int P, int D, const float* cos_t,
                        const float* sin_t, hipStream_t s);
 hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t s);
+
+// ---- SPARC head training (sparc_train.hip) ----
+// LayerNorm (eps 1e-5) + Dropout(p) per row of D (% 256, <= 1024): out bf16 or f32, stats[r] = (mu, rstd);
+// the keep mask is a counter hash of (seed, r * D + c), recomputed by launch_ln_grad
+hipError_t launch_ln_drop(const float* x, const float* w, const float* b, long R, int D, float p, uint64_t seed,
+                          void* out, bool out_bf16, float2* stats, hipStream_t s);
+// dw, db (overwritten) = the LayerNorm weight / bias gradients through that dropout; scratch >= ln_grad_scratch_floats
+long ln_grad_scratch_floats(long R, int D);
+hipError_t launch_ln_grad(const float* dy, const float* x, const float2* stats, long R, int D, float p, uint64_t seed,
+                          float* dw, float* db, float* scratch, hipStream_t s);
+// io: d loss / d W in, d loss / d S out, per row of P (sparc weights backward, S = raw similarity)
+hipError_t launch_align_bwd(const float* S, float* io, long rows, int P, float sigma, hipStream_t s);
+// SparcLoss local-term gradient per sample: dR, dR^T [B][T][T] and part[B][3] from R = scale Gn Ln^T (T <= 80)
+hipError_t launch_local_grad(const float* R, const float* mask, int B, int T, float w, float* dR, float* dRT,
+                             float* part, hipStream_t s);
+// g = w (softmax(z) - onehot(row)), loss[row] = lse - z[row]
+hipError_t launch_ce_diag_grad(const float* z, int R, int C, float w, float* g, float* loss, hipStream_t s);
+// out[z][c][r] = in[z][r][c] (+ add[z][c][r])
+hipError_t launch_transpose_add(const float* in, const float* add, float* out, int batch, int R, int C, hipStream_t s);
+// x[b][p][d] += scale * v[b][d]
+hipError_t launch_bcast_add_mid(float* x, const float* v, int B, int P, int D, float scale, hipStream_t s);
 
 // SparcLoss pieces (pacl.py:516-584)
 hipError_t launch_mean_mid(float* out, const float* x, int B, int P, int D, hipStream_t s);   // mean over dim 1

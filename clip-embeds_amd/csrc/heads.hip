@@ -73,7 +73,8 @@ __global__ __launch_bounds__(256) void fgemm_k(FGemmParams p) {
     for (int r = 0; r < 16; ++r) {
         const int gi = i0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (gi >= p.M) continue;
-        const float v = acc[r] * p.alpha + bj;
+        float v = acc[r] * p.alpha + bj;
+        if (p.accumulate) v += C[(size_t)gi * p.ldc + gj];
         C[(size_t)gi * p.ldc + gj] = v;
         if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
     }
@@ -184,7 +185,8 @@ __global__ __launch_bounds__(256) void fgemm2_k(FGemmParams p) {
         for (int e = 0; e < 16; ++e) {
             const int gi = i0 + r * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
             if (gi >= p.M) continue;
-            const float v = acc[r][e] * p.alpha + bj;
+            float v = acc[r][e] * p.alpha + bj;
+            if (p.accumulate) v += C[(size_t)gi * p.ldc + gj];
             C[(size_t)gi * p.ldc + gj] = v;
             if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
         }
@@ -299,7 +301,8 @@ __global__ __launch_bounds__(256) void fgemm3_k(FGemmParams p) {
             for (int r = 0; r < 4; ++r) {
                 const int gi = i0 + ib * 16 + 4 * g + r;
                 if (gi >= p.M) continue;
-                const float v = acc[ib][jb][r] * p.alpha + bj;
+                float v = acc[ib][jb][r] * p.alpha + bj;
+                if (p.accumulate) v += C[(size_t)gi * p.ldc + gj];
                 C[(size_t)gi * p.ldc + gj] = v;
                 if (p.Ct) p.Ct[(size_t)gj * p.ldct + gi] = v;
             }

@@ -262,6 +262,44 @@ int ce_contrastive_loss_partial(ce_handle* h, void* stream, const float* img_all
 int ce_loss_combine(ce_handle* h, void* stream, const float* parts, int n_global, float global_weight,
                     float local_weight, float* out_loss);
 
+/* SPARC head training step (Patch-Aligned-Contrastive-Learning/train_sparc.py:29-37,91,106 on
+ * model/pacl.py:380-584: sparc / sparc_rope forward in train mode, SparcLoss(temperature), loss.backward(),
+ * torch.optim.Adam over the heads; the CLIP towers are frozen, pacl.py:408).  The caller owns f32 master
+ * values and gradient slots of the 12 head tensors (visual_projection.0.{weight,bias},
+ * .2.linear_projection.0.*, .2.non_linear_projection.{0,2}.*, text_projection.0.*, text_projection.2.*) and
+ * runs the optimizer (ce_adamw with weight_decay 0 is torch.optim.Adam).  Data-parallel ranks follow the
+ * reference's nn.DataParallel semantics (the loss over the WHOLE gathered batch, gradients summed over
+ * replicas) through the same collectives as the value path above.
+ *   ce_sparc_train_bind          params / grads: the 12 head tensors by name (f32 device buffers)
+ *   ce_sparc_train_sync_weights  engine compute copies of the heads <- masters (after each update)
+ *   ce_sparc_train_forward       patch_tokens f32 [B,P,Dv] (visual.output_tokens, ln_post'd), rope:
+ *                                CE_ROPE_BEFORE (sparc_rope) or NONE; text f32 [B,T,E] = the text tower's
+ *                                tokens (text_mode 0: through text_projection) or the token embeddings
+ *                                themselves (text_mode 1: precomputed / LLM embeddings, no text head);
+ *                                Dropout(dropout) after both head LayerNorms with masks from a counter
+ *                                hash of seed (dropout 0: eval-mode heads).  Keeps every activation the
+ *                                backward needs; out_v [B,P,Pd], out_l [B,T,Pd] (normalised), out_g
+ *                                [B,T,Pd] (normalised grouped patches) as sparc.forward returns them
+ *                                (each nullable).  T <= 80.
+ *   ce_sparc_train_loss_grad     after ce_sparc_loss_means(out_v, out_l) and the all-gather of those
+ *                                means (img_all / txt_all [Bg,Pd], this rank's rows at row0): parts[5]
+ *                                (as ce_sparc_loss_partial, for ce_loss_combine after the all-reduce) and
+ *                                the gradient of the global loss w.r.t. this rank's means and local-term
+ *                                inputs (kept in the handle); mask f32 [B,T]; mask_total = the mask's sum
+ *                                over the global batch (the local term's divisor).
+ *   ce_sparc_train_backward      every bound gradient slot (overwritten; the text head's are zeroed with
+ *                                text_mode 1) from those gradients through the alignment, the heads, the
+ *                                dropouts and the head LayerNorms. */
+int ce_sparc_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* grads, int n);
+int ce_sparc_train_sync_weights(ce_handle* h, void* stream);
+int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens, int B, int P, int rope,
+                           const float* text, int text_mode, int T, float sigma, float dropout, uint64_t seed,
+                           float* out_v, float* out_l, float* out_g);
+int ce_sparc_train_loss_grad(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg, int row0,
+                             const float* mask, float mask_total, float temperature, float global_weight,
+                             float local_weight, float* parts);
+int ce_sparc_train_backward(ce_handle* h, void* stream);
+
 /* apply_rope (pacl.py:147-181): de-interleaving rotary embedding over positions 0..P-1.
  * x, out: device f32 [B,P,D] (may alias). */
 int ce_apply_rope(ce_handle* h, void* stream, const float* x, int B, int P, int D, float* out);
