@@ -17,8 +17,10 @@ Workloads (BASELINE.json configs; a "step" is one pass of the hot path over one 
            as train_pacl.py:34-36 computes it after nn.DataParallel's gather).
   negclip  (configs[3]) NegCLIP training step, locked image tower: 1024 pairs + 512 hard-negative
            captions per GPU, text tower backward, RCCL all-reduce of text gradients, AdamW.
-  sparc    (configs[4]) SPARC with precomputed text-token embeddings [B,77,768] + mask: image
-           tower + patch head, patch x token similarity / alignment (pacl.py:455-478) and SparcLoss
+  sparc    (configs[4]) the train_sparc.py step with precomputed text-token embeddings [B,77,768] +
+           mask: frozen image tower, patch head in train mode (Dropout 0.1), patch x token similarity /
+           alignment (pacl.py:455-478), SparcLoss, head backward and Adam (--sparc-forward: forward + loss
+           value only); SparcLoss
            (pacl.py:516-584, temperature 0.1 as train_sparc.py:105; N > 1: RCCL all-gather of the
            [B,768] normalised patch / token means for the global term, the per-sample local term's sums
            and the global CE sums all-reduced: the loss over the whole global batch, as
@@ -327,23 +329,39 @@ def build_sparc(args, dev, rank, world):
     l_tok = (torch.randn(B, T, D, generator=g) * 0.5).to(dev)
     eot = torch.randint(6, 42, (B,), generator=g)
     mask = (torch.arange(T).expand(B, -1) <= eot[:, None]).float().to(dev)
-    loss_fn = SparcLoss(0.1, engine=mod.engine, rank=rank, world_size=world)     # train_sparc.py:105
-
-    def step():
-        v = mod.forward_visual(imgs)
-        gr, ln = mod.align(v, l_tok)
-        return loss_fn(v, ln, gr, mask)
-
     sim_flops = 2.0 * T * P * D
-    cfgd = {"workload": f"SPARC ({cls.__name__}) image tower + patch head, patch x token similarity / alignment, "
-                        "SparcLoss with precomputed text-token embeddings (BASELINE configs[4]: batch 256/GPU)",
+    fwd_flops = IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D
+    if args.sparc_forward:
+        loss_fn = SparcLoss(0.1, engine=mod.engine, rank=rank, world_size=world)     # train_sparc.py:105
+
+        def step():
+            v = mod.forward_visual(imgs)
+            gr, ln = mod.align(v, l_tok)
+            return loss_fn(v, ln, gr, mask)
+        flops, what = fwd_flops, "forward + SparcLoss value"
+    else:
+        # the train_sparc.py:29-37 step: frozen image tower, heads in train mode (Dropout 0.1), SparcLoss,
+        # backward through the alignment and the patch head, Adam(lr 1e-4) (train_sparc.py:91,106)
+        tr = clipembed.SparcHeadTrainer(mod, lr=1e-4, dropout=0.1, temperature=0.1, rank=rank, world_size=world)
+
+        def step():
+            loss = tr.compute_grads(imgs, l_token_embed=l_tok, language_mask=mask)
+            tr.apply_update()
+            return loss
+        # backward: weight gradients of the head (1x its forward; the hidden layer's input gradient adds
+        # ~0.5x) and both operand gradients of the similarity / grouping products (2x)
+        flops = fwd_flops + 1.5 * PACL_HEAD_FLOPS + 2 * (2 * sim_flops)
+        what = "training step: forward (dropout 0.1) + SparcLoss + head backward + Adam"
+    cfgd = {"workload": f"SPARC ({cls.__name__}) {what}: image tower + patch head, patch x token similarity / "
+                        "alignment, SparcLoss with precomputed text-token embeddings (BASELINE configs[4]: batch 256/GPU)",
             "batch_per_gpu": B, "global_batch": world * B, "tokens": T, "patches": P, "dim": D,
             "parallelism": f"dp{world}", "loss_temperature": 0.1,
             "exchange": ("RCCL all_gather of the normalised patch / token means [B,768] x2 + all_reduce of the "
-                         "5 loss partial sums (global-batch SparcLoss value)") if world > 1 else "none"}
-    return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg,
-                flops_per_pair=IMAGE_FLOPS + PACL_HEAD_FLOPS + 2 * sim_flops + 2.0 * T * T * D, prunable=False,
-                metric="SPARC image-text pairs/sec ViT-L/14-336", config=cfgd)
+                         "5 loss partial sums" + ("" if args.sparc_forward else " + all_reduce of the head gradients")
+                         ) if world > 1 else "none"}
+    return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg, flops_per_pair=flops, prunable=False,
+                metric="SPARC image-text pairs/sec ViT-L/14-336" + ("" if args.sparc_forward else " (training)"),
+                config=cfgd)
 
 
 BUILDERS = {"clip": build_clip, "pacl": build_pacl, "negclip": build_negclip, "sparc": build_sparc}
@@ -380,6 +398,8 @@ def main():
     ap.add_argument("--hard", type=int, default=None, help="negclip: hard-negative captions per GPU (default B/2)")
     ap.add_argument("--pacl-mode", choices=["ones", "sigmoid_rope_after"], default="ones")
     ap.add_argument("--sparc-rope", action="store_true")
+    ap.add_argument("--sparc-forward", action="store_true",
+                    help="sparc: time the forward + loss value only (default: the full training step)")
     ap.add_argument("--cpu-batch", type=int, default=8, help="pairs per CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")

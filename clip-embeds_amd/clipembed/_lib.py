@@ -124,6 +124,7 @@ _SIGNATURES = {
     "ce_train_sync_weights": (c_int, [c_void_p, c_void_p]),
     "ce_text_forward_train": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "ce_text_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int]),
+    "ce_text_backward_events": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int]),
     "ce_contrastive_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p,
                                     c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "ce_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,

@@ -241,11 +241,14 @@ def _all_gather_rows(x: torch.Tensor, world_size: int, rank: int):
 
 
 def _value_only(name: str, *tensors):
-    """The sharded losses return the reference's global VALUE (logging, evaluation); their all-gather
-    is not differentiable, so a caller that needs gradients must not get a silently detached loss."""
+    """The engine's losses return the reference's VALUE (logging, evaluation): no autograd runs through
+    the engine (nor through the sharded path's all-gather), so a caller that needs gradients must not
+    get a silently detached loss.  Training goes through the trainers, which compute the gradients in
+    the engine: clipembed.SparcHeadTrainer (train_sparc.py's step), clipembed.TextTowerTrainer (NegCLIP)."""
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
-        raise RuntimeError(f"{name}(rank=, world_size=) returns the global loss value only (no autograd "
-                           "through the all-gather); call it under torch.no_grad() or on detached inputs")
+        raise RuntimeError(f"{name} returns the loss value only (no autograd through the engine); call it under "
+                           "torch.no_grad() or on detached inputs, and train with clipembed.SparcHeadTrainer / "
+                           "TextTowerTrainer")
 
 
 def _all_reduce_sum(x: torch.Tensor) -> torch.Tensor:
@@ -264,9 +267,9 @@ class ClipLoss(torch.nn.Module):
     outputs to one device.  The ranks all-gather the [B_r, D] features (B_r may differ per rank:
     sizes first, padded rows), each takes the CE sums of its own rows of the global logits both ways
     (ce_contrastive_loss_partial), one all-reduce adds them, ce_loss_combine divides by the global
-    batch.  Every rank returns the same value.  The sharded path returns the VALUE only (the
-    all-gather is not differentiable): with inputs that require grad it raises instead of returning
-    a detached loss; the single-process path is @no_grad as before (the engine computes no autograd)."""
+    batch.  Every rank returns the same value.  Both paths return the VALUE only (the engine runs no
+    autograd, nor does the all-gather): with inputs that require grad they raise instead of returning
+    a detached loss (_value_only; gradients: clipembed.SparcHeadTrainer / TextTowerTrainer)."""
 
     def __init__(self, temperature: float, engine=None, rank: int = 0, world_size: int = 1):
         super().__init__()
@@ -312,8 +315,7 @@ class ClipLoss(torch.nn.Module):
         return out
 
     def forward(self, image_features, text_features):
-        if self.world_size > 1:
-            _value_only("ClipLoss", image_features, text_features)
+        _value_only("ClipLoss", image_features, text_features)
         with torch.no_grad():
             return self._forward(image_features, text_features)
 
@@ -366,8 +368,7 @@ class SparcLoss(ClipLoss):
         return parts
 
     def forward(self, v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask):
-        if self.world_size > 1:
-            _value_only("SparcLoss", v_patch_embed, l_token_embed, l_grouped_v_patch_embed)
+        _value_only("SparcLoss", v_patch_embed, l_token_embed, l_grouped_v_patch_embed)
         with torch.no_grad():
             return self._forward(v_patch_embed, l_token_embed, l_grouped_v_patch_embed, language_mask)
 

@@ -14,7 +14,11 @@ open_clip/src/train-clip.sh (`--lock-image --local-loss --gather-with-grad [--us
      every rank's gradient of this rank's rows) is an RCCL reduce_scatter of d(all text features),
      laid out in the gather's padded per-rank chunks;
   5. text-tower backward into one flat f32 gradient buffer (ce_text_backward), DDP's gradient
-     all-reduce as ONE RCCL all_reduce(AVG) of that buffer (main.py:302);
+     all-reduce (main.py:302) bucketed as DDP does: ce_text_backward_events records an event as each
+     bucket of blocks (top-down) has its final gradients, and each bucket's all_reduce(SUM) runs on
+     a side stream behind its event while the blocks below are still in their backward; the sum is
+     divided by the world size once all buckets are in (`bucket_blocks` blocks per bucket, 0 = one
+     all_reduce of the whole buffer after the backward);
   6. AdamW on the flat f32 masters, two groups as main.py:335-349 (gain/bias/ln/logit_scale
      without weight decay), then the engine's compute copies are refreshed from the masters
      (ce_train_sync_weights) and logit_scale is clamped to [0, ln 100] (train.py:189).
@@ -118,7 +122,7 @@ class TextTowerTrainer:
 
     def __init__(self, model: CLIP, lr: float = 5e-6, betas=(0.9, 0.98), eps: float = 1e-6,
                  weight_decay: float = 0.0, local_loss: bool = True, gather_with_grad: bool = True,
-                 usehardtext: bool = False, rank: int = 0, world_size: int = 1):
+                 usehardtext: bool = False, rank: int = 0, world_size: int = 1, bucket_blocks: int = 1):
         if world_size > 1 and not (local_loss and gather_with_grad):
             raise NotImplementedError("the engine implements the train-clip.sh setting: --local-loss --gather-with-grad")
         self.model = model
@@ -165,6 +169,39 @@ class TextTowerTrainer:
         self.lossbuf = torch.zeros(2, device=self.dev, dtype=torch.float32)
         self.overlap_text = False           # text forward beside the image forward (compute_grads)
         self._side = None
+        self._ar_side = None
+        self.bucket_blocks = bucket_blocks
+        self._buckets = self._make_buckets(bucket_blocks) if world_size > 1 and bucket_blocks > 0 else None
+
+    def _runs(self, names, extra=()):
+        """Contiguous [lo, hi) element ranges of the flat gradient buffer covering `names` (+ extra)."""
+        base = self.grad.storage_offset()
+        iv = sorted([(self.gviews[n].storage_offset() - base, self.gviews[n].storage_offset() - base +
+                      self.gviews[n].numel()) for n in names] + list(extra))
+        runs = [list(iv[0])]
+        for lo, hi in iv[1:]:
+            if lo == runs[-1][1]:
+                runs[-1][1] = hi
+            else:
+                runs.append([lo, hi])
+        return [tuple(r) for r in runs]
+
+    def _make_buckets(self, per: int):
+        """[(event index or None, runs)] in the order the backward finishes them: the head (+ logit_scale),
+        groups of `per` blocks top-down (event after the group's lowest block), the embeddings (end)."""
+        nl = self.model.cfg.text.layers
+        n = self.n_total
+        out = [(0, self._runs(["ln_final.weight", "ln_final.bias", "text_projection"], [(n - 1, n)]))]
+        blocks = list(range(nl - 1, -1, -1))
+        for i in range(0, nl, per):
+            grp = blocks[i:i + per]
+            names = [nm for b in grp for nm in self.gviews if nm.startswith(f"transformer.resblocks.{b}.")]
+            out.append((1 + (nl - 1 - grp[-1]), self._runs(names)))
+        out.append((None, self._runs(["token_embedding.weight", "positional_embedding"])))
+        covered = sum(hi - lo for _, runs in out for lo, hi in runs)
+        if covered != n:
+            raise RuntimeError(f"gradient buckets cover {covered} of {n} elements")
+        return out
 
     # ------------------------------------------------------------------ pieces
     @property
@@ -227,12 +264,48 @@ class TextTowerTrainer:
         """Steps 3-5 given both towers' features (txt from ce_text_forward_train on this handle)."""
         scale = math.exp(float(self.logit_scale))
         dtxt = self.loss_and_feature_grad(img, txt, scale)
+        if self.world > 1 and self._buckets is not None:
+            self._backward_bucketed(dtxt, txt.shape[0])
+            return self.lossbuf[0].clone()
         _lib.call("ce_text_backward", self.e.h, _stream(self.dev), _ptr(dtxt), txt.shape[0])
         self.grad[-1:].copy_(self.lossbuf[1:2])       # d loss / d logit_scale
         if self.world > 1:                            # DDP: average over ranks, one flat buffer
             dist.all_reduce(self.grad)
             self.grad.div_(self.world)
         return self.lossbuf[0].clone()
+
+    def _backward_bucketed(self, dtxt: torch.Tensor, T: int):
+        """Step 5 with DDP's overlap: bucket k's all_reduce is enqueued on a side stream behind the
+        event the backward records when that bucket's gradients are final."""
+        main = torch.cuda.current_stream(self.dev)
+        if self._ar_side is None:
+            self._ar_side = torch.cuda.Stream(device=self.dev)
+            nl = self.model.cfg.text.layers
+            self._events = [None] * (nl + 1)
+            for ev_i, _ in self._buckets:
+                if ev_i is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(main)                   # creates the event (re-recorded by the engine)
+                    self._events[ev_i] = ev
+            self._ev_ptrs = (ctypes.c_void_p * (nl + 1))(
+                *[ctypes.c_void_p(ev.cuda_event) if ev is not None else None for ev in self._events])
+        side = self._ar_side
+        self.grad[-1:].copy_(self.lossbuf[1:2])       # d loss / d logit_scale (the head bucket)
+        _lib.call("ce_text_backward_events", self.e.h, _stream(self.dev), _ptr(dtxt), T, self._ev_ptrs,
+                  len(self._ev_ptrs))
+        works = []
+        with torch.cuda.stream(side):
+            for ev_i, runs in self._buckets:
+                if ev_i is None:
+                    side.wait_stream(main)            # the embeddings: the end of the backward
+                else:
+                    side.wait_event(self._events[ev_i])
+                for lo, hi in runs:
+                    works.append(dist.all_reduce(self.grad[lo:hi], async_op=True))
+        for w in works:
+            w.wait()                                  # the current (main) stream waits for the sums
+        main.wait_stream(side)
+        self.grad.div_(self.world)
 
     def apply_update(self, lr: Optional[float] = None):
         """Step 6: AdamW on both groups, logit_scale clamp, engine weights refreshed."""

@@ -1039,7 +1039,16 @@ int run_text_train(ce_handle* h, hipStream_t s, TrainWs& w, const int64_t* ids) 
 }
 
 // d(loss)/d(every bound text tensor) from d(loss)/d(normalised features) [B][E]
-int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfeat) {
+// events (optional, n_events = layers + 1; null entries skipped): events[0] is recorded once the head's
+// gradients (ln_final, text_projection) are final, events[1 + i] once block layers - 1 - i's are, so a
+// caller can all-reduce each bucket of blocks on another stream while the blocks below run (DDP's
+// bucketed overlap, main.py:302); the embeddings' gradients are final when the stream reaches the end
+int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfeat, void* const* events = nullptr,
+                      int n_events = 0) {
+    auto mark = [&](int i) -> int {
+        if (events && i < n_events && events[i]) HIP_TRY(hipEventRecord((hipEvent_t)events[i], s));
+        return CE_OK;
+    };
     const ce_config& c = h->cfg;
     const int D = w.D, F = w.F, E = w.E, L = c.context_length, H = c.text.heads, M = w.M, Mp = w.Mp, B = w.B;
     const int act = act_code(h);
@@ -1064,6 +1073,7 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
     CE_TRY(timed(h, s, "t_ln_final_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[w.nl], w.dpool, D, W(h, "ln_final.weight"), w.rows, B, D,
                                           grad_of(h, "ln_final.weight"), grad_of(h, "ln_final.bias"), false, false,
                                           w.lnscr, s, w.dres_b, grad_of(h, top + "mlp.c_proj.bias")); }));
+    CE_TRY(mark(0));
     const float qs = ce::kAttnQScale;
     // MN-major dW GEMMs: widths that are multiples of 256 (ViT-B/L text towers: 512, 768) and
     // activations under the kernel's 32-bit DMA offsets (< 2 GB: up to ~340k token rows at F = 3072);
@@ -1153,6 +1163,7 @@ int run_text_backward(ce_handle* h, hipStream_t s, TrainWs& w, const float* dfea
         float* below = l > 0 ? grad_of(h, "transformer.resblocks." + std::to_string(l - 1) + ".mlp.c_proj.bias") : nullptr;
         CE_TRY(timed(h, s, "t_ln_1_bwd", 0.0, 0.0, [&] { return ce::launch_ln_bwd(w.dres, w.X[l], nullptr, D, k.ln1w, nullptr, M, D, G("ln_1.weight"),
                                               G("ln_1.bias"), true, false, w.lnscr, s, w.dres_b, below, dxb); }));
+        CE_TRY(mark(w.nl - l));
     }
     // token / positional embeddings (model.py:286-288)
     CE_TRY(timed(h, s, "t_embed_bwd", 0.0, 0.0, [&] { return ce::launch_embed_bwd(grad_of(h, "token_embedding.weight"), grad_of(h, "positional_embedding"),
@@ -2704,6 +2715,23 @@ int ce_text_backward(ce_handle* h, void* stream, const float* d_features, int B)
     TrainWs w;
     train_layout(h, B, &w, h->tr);
     return run_text_backward(h, s, w, d_features);
+}
+
+int ce_text_backward_events(ce_handle* h, void* stream, const float* d_features, int B, void* const* events,
+                            int n_events) {
+    if (!h || !d_features) return fail(CE_ERR_INVALID, "ce_text_backward_events: null argument");
+    if (h->bound.empty()) return fail(CE_ERR_STATE, "ce_text_backward_events: no gradient buffers bound (ce_train_bind)");
+    if (B != h->tr_B || B <= 0)
+        return fail(CE_ERR_STATE, "ce_text_backward_events: batch %d does not match the last ce_text_forward_train (%d)",
+                    B, h->tr_B);
+    if (n_events < 0 || (n_events > 0 && !events) || n_events > h->cfg.text.layers + 1)
+        return fail(CE_ERR_INVALID, "ce_text_backward_events: %d events for %d blocks (at most layers + 1)", n_events,
+                    h->cfg.text.layers);
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    TrainWs w;
+    train_layout(h, B, &w, h->tr);
+    return run_text_backward(h, s, w, d_features, events, n_events);
 }
 
 int ce_contrastive_grad(ce_handle* h, void* stream, const float* A, int Ra, const float* Bm, int Cb, int E, float scale,

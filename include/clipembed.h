@@ -462,6 +462,14 @@ int ce_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* grads,
 int ce_train_sync_weights(ce_handle* h, void* stream);
 int ce_text_forward_train(ce_handle* h, void* stream, const int64_t* ids, int B, float* out_features);
 int ce_text_backward(ce_handle* h, void* stream, const float* d_features, int B);
+/* ce_text_backward that also records hipEvent_t events[i] (n_events <= text layers + 1, null entries
+ * skipped) on the stream as the gradients become final: events[0] after the head (ln_final,
+ * text_projection), events[1 + i] after block (layers - 1 - i), the blocks running top-down; the
+ * token / positional embeddings are final at the end.  Lets the caller all-reduce finished buckets of
+ * blocks on another stream while the lower blocks' backward runs (DDP's bucketed overlap,
+ * open_clip_train/main.py:302). */
+int ce_text_backward_events(ce_handle* h, void* stream, const float* d_features, int B, void* const* events,
+                            int n_events);
 int ce_contrastive_grad(ce_handle* h, void* stream, const float* A, int Ra, const float* B, int Cb, int E, float scale,
                         const int64_t* labels, float weight, float inv_count, float* out2, float* dA, float* dB);
 int ce_adamw(void* stream, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,

@@ -162,3 +162,81 @@ def test_loss_decreases(b16):
     tr = clipembed.SparcHeadTrainer(b16["m"], lr=1e-4, dropout=0.1)
     losses = [tr.step(b16["imgs"], b16["caps"]) for _ in range(4)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+
+# ------------------------------------------------------------------------------- two ranks (gloo)
+def _dist_inputs(r):
+    gen = torch.Generator(device="cpu").manual_seed(40 + r)
+    l_tok = torch.randn(3, 77, 768, generator=gen) * 0.5
+    eot = torch.randint(6, 42, (3,), generator=gen)
+    mask = (torch.arange(77)[None, :] <= eot[:, None]).float()
+    return W.synthetic_images(3, seed=1600 + r), l_tok, mask
+
+
+def _dist_trainer(world, rank):
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    m = _model(sparc_rope, cfg, W.synthetic_state_dict(cfg))
+    return clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0, rank=rank, world_size=world)
+
+
+def _dist_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        imgs, l_tok, mask = _dist_inputs(rank)
+        tr = _dist_trainer(world, rank)
+        before = tr.param.clone()
+        loss = tr.compute_grads(torch.from_numpy(imgs).cuda(), l_token_embed=l_tok.cuda(), language_mask=mask.cuda())
+        tr.apply_update()
+        torch.cuda.synchronize()
+        q.put((rank, {"loss": float(loss), "grad": tr.grad.cpu().numpy(), "upd": (tr.param - before).cpu().numpy()}))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_equal_one_rank_on_concatenated_batch():
+    """BASELINE configs[4]'s exchange (train_sparc.py:93: nn.DataParallel, the loss over the gathered
+    batch, the replicas' gradients summed): two spawned ranks on cuda:0 over gloo (RCCL on the
+    driver's multi-GPU node), 3 samples each, against one rank on the 6 concatenated samples: the same
+    loss, the same summed gradient and the same first Adam step on both ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    ins = [_dist_inputs(r) for r in range(2)]
+    tr = _dist_trainer(1, 0)
+    before = tr.param.clone()
+    loss1 = float(tr.compute_grads(torch.from_numpy(np.concatenate([i[0] for i in ins])).cuda(),
+                                   l_token_embed=torch.cat([i[1] for i in ins]).cuda(),
+                                   language_mask=torch.cat([i[2] for i in ins]).cuda()))
+    g1 = tr.grad.cpu().numpy()
+    tr.apply_update()
+    u1 = (tr.param - before).cpu().numpy()
+    del tr
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=300) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for r in range(2):
+        np.testing.assert_allclose(got[r]["loss"], loss1, rtol=1e-4)
+        assert _cos(got[r]["grad"], g1) > 0.9999, r
+        np.testing.assert_allclose(np.linalg.norm(got[r]["grad"]), np.linalg.norm(g1), rtol=2e-3)
+        np.testing.assert_array_equal(got[r]["grad"], got[0]["grad"])
+        np.testing.assert_array_equal(got[r]["upd"], got[0]["upd"])
+        big = np.abs(g1) > 0.1 * np.abs(g1).max()
+        np.testing.assert_allclose(got[r]["upd"][big], u1[big], rtol=2e-3, atol=1e-9)

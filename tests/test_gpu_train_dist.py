@@ -10,7 +10,8 @@ runs one rank per device; the driver's 8-GPU run uses RCCL) and run the engine:
   * feature level: negclip_feature_grad with the engine's ce_contrastive_grad on the reference's
     2-rank inputs, against the reference's own 2-rank autograd (tests/golden/train_dist.npz: loss,
     d loss / d scale, d loss / d text features per rank);
-  * whole step: TextTowerTrainer(rank, world_size=2) on 3 images + 3 / 2 captions per rank (hard
+  * whole step (with the bucketed, backward-overlapped gradient all-reduce and with one all-reduce
+    after the backward): TextTowerTrainer(rank, world_size=2) on 3 images + 3 / 2 captions per rank (hard
     negatives of different counts, so the size gather and padding are exercised), against one
     TextTowerTrainer(world_size=1) on the concatenated batch [originals r0, originals r1, hard r0,
     hard r1]: data parallelism must not change the step, so the DDP-averaged gradient equals the
@@ -133,7 +134,7 @@ def _inputs():
     return imgs, caps
 
 
-def _trainer(world, rank):
+def _trainer(world, rank, bucket_blocks=1):
     import clipembed
     from clipembed import weights as W
     from clipembed.config import get_model_config
@@ -141,7 +142,8 @@ def _trainer(world, rank):
     m = clipembed.CLIP(cfg)
     m.load_state_dict(W.synthetic_state_dict(cfg))
     m.to("cuda")
-    return clipembed.TextTowerTrainer(m, lr=5e-6, usehardtext=True, rank=rank, world_size=world)
+    return clipembed.TextTowerTrainer(m, lr=5e-6, usehardtext=True, rank=rank, world_size=world,
+                                      bucket_blocks=bucket_blocks)
 
 
 def _summary(tr, loss, before, idx):
@@ -154,11 +156,11 @@ def _summary(tr, loss, before, idx):
             "dls": float(g[-1]), "u_ls": float(upd[-1])}
 
 
-def _step_worker(rank, world, port, q, idx):
+def _step_worker(rank, world, port, q, idx, bucket_blocks):
     dist, staged = _setup(rank, world, port)
     try:
         imgs, caps = _inputs()
-        tr = _trainer(world, rank)
+        tr = _trainer(world, rank, bucket_blocks)
         before = tr.param.clone()
         loss = tr.compute_grads(torch.from_numpy(imgs[rank]).cuda(), torch.from_numpy(caps[rank]).cuda())
         tr.apply_update()
@@ -177,7 +179,10 @@ def _cos(a, b):
     return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
 
 
-def test_negclip_step_two_ranks_equals_one_rank_on_concatenated_batch():
+@pytest.mark.parametrize("bucket_blocks", [1, 0])
+def test_negclip_step_two_ranks_equals_one_rank_on_concatenated_batch(bucket_blocks):
+    """bucket_blocks 1: the per-block bucketed all-reduce overlapped with the backward (the default);
+    0: one all-reduce of the whole buffer after it."""
     imgs, caps = _inputs()
     tr = _trainer(1, 0)
     n = tr.n_total
@@ -194,7 +199,7 @@ def test_negclip_step_two_ranks_equals_one_rank_on_concatenated_batch():
     del tr
     torch.cuda.empty_cache()
 
-    got = _spawn(_step_worker, (idx,))
+    got = _spawn(_step_worker, (idx, bucket_blocks))
     print("reduce_scatter on device tensors:", "host-staged (gloo)" if got[0]["staged"] else "gloo native")
     # the mean of the two local losses is the global loss
     np.testing.assert_allclose((got[0]["loss"] + got[1]["loss"]) / 2, one["loss"], rtol=2e-4)
