@@ -97,6 +97,13 @@ struct FoldOps {
     }
 };
 
+// cache policy of the GEMM epilogues' output stores (buffer-store aux bits; gfx950: 1 = sc0, 2 = nt,
+// 16 = sc1).  0 = plain (the line stays in the XCD's L2); an A/B build with 16 (sc1: written through
+// and dropped from the L2) leaves the L2 to the operand panels
+#ifndef CE_STORE_AUX
+#define CE_STORE_AUX 0
+#endif
+
 #ifndef CE_FOLD_PREFETCH
 #define CE_FOLD_PREFETCH 0
 #endif
@@ -453,13 +460,13 @@ __device__ __forceinline__ void w4_epilogue_bf16_n(const GemmParams& p, const f3
             const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
             const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
             const u32x4 d = {x[0], y[0], x[1], y[1]};
-            __builtin_amdgcn_raw_buffer_store_b128(d, osrd, voff + j * 32, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(d, osrd, voff + j * 32, 0, CE_STORE_AUX);
             if constexpr (MAYPRE) {
                 if (pre) {
                     const auto px = __builtin_amdgcn_permlane16_swap(hp[0].x, hp[1].x, false, false);
                     const auto py = __builtin_amdgcn_permlane16_swap(hp[0].y, hp[1].y, false, false);
                     const u32x4 dp = {px[0], py[0], px[1], py[1]};
-                    __builtin_amdgcn_raw_buffer_store_b128(dp, psrd, voff + j * 32, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(dp, psrd, voff + j * 32, 0, CE_STORE_AUX);
                 }
             }
         }
@@ -542,7 +549,7 @@ __device__ __forceinline__ void w4_epilogue_act_bwd(const GemmParams& p, const f
             const auto x = __builtin_amdgcn_permlane16_swap(h[0].x, h[1].x, false, false);
             const auto y = __builtin_amdgcn_permlane16_swap(h[0].y, h[1].y, false, false);
             const u32x4 o = {x[0], y[0], x[1], y[1]};
-            __builtin_amdgcn_raw_buffer_store_b128(o, osrd, voff0 + ip * 32 * ldo2 + j * 32, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(o, osrd, voff0 + ip * 32 * ldo2 + j * 32, 0, CE_STORE_AUX);
         }
     }
     // column c = 16j + 4fq + e of value k = 4j + e; after the four steps lane fr holds k = 2fr, 2fr + 1
@@ -607,7 +614,7 @@ __device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 
             f32x4 v = acc[i][j];
             const f32x4 r = rv[i % RD][j];
             v[0] += bv[j].x + r[0]; v[1] += bv[j].y + r[1]; v[2] += bv[j].z + r[2]; v[3] += bv[j].w + r[3];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), os, ooff + j * 64, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), os, ooff + j * 64, 0, CE_STORE_AUX);
             // Chan's pairwise update: the 4 values of block j join the lane's 4jj earlier ones
             const float m4 = ((v[0] + v[1]) + (v[2] + v[3])) * 0.25f;
             const float d0 = v[0] - m4, d1 = v[1] - m4, d2 = v[2] - m4, d3 = v[3] - m4;
@@ -628,7 +635,7 @@ __device__ __forceinline__ void epi_stats_rows(const GemmParams& p, const f32x4 
                 const auto x = __builtin_amdgcn_permlane16_swap(pxb[j].x, o.x, false, false);
                 const auto y = __builtin_amdgcn_permlane16_swap(pxb[j].y, o.y, false, false);
                 const u32x4 d = {x[0], y[0], x[1], y[1]};
-                __builtin_amdgcn_raw_buffer_store_b128(d, xs, xoff + j * 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(d, xs, xoff + j * 32, 0, CE_STORE_AUX);
             }
         }
         ooff += ostep;
@@ -1600,8 +1607,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_resid_hl(GemmParams p) {
                 const auto yy = __builtin_amdgcn_permlane16_swap(l[0].y, l[1].y, false, false);
                 const u32x4 dh = {x[0], y[0], x[1], y[1]};
                 const u32x4 dl = {xx[0], yy[0], xx[1], yy[1]};
-                __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(dh, xs, xo + j * 32, 0, CE_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(dl, xl, xo + j * 32, 0, CE_STORE_AUX);
             }
             xo += 32 * ldo * 2;
 #pragma unroll
