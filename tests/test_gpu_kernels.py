@@ -285,10 +285,10 @@ def attn_ref(qkv, B, L, H, causal):
     return (p @ v).permute(0, 2, 1, 3).reshape(B * L, D)
 
 
-@pytest.fixture(params=[125, 381], ids=lambda v: f"attn_var{v}")
+@pytest.fixture(params=[125, 381, 1125, 1381], ids=lambda v: f"attn_var{v}")
 def attn_var(request):
-    """Both attention forward variants (ce_set_attn_variant) against torch f32 (causal
-    launches run the general-path kernel under either)."""
+    """The attention forward variants (ce_set_attn_variant, DESIGN.md §6.6, §6.19: 1xxx = two 32-query
+    sets per wave) against torch f32 (causal launches run the general-path kernel under any)."""
     prev = _lib.lib().ce_set_attn_variant(request.param)
     yield request.param
     _lib.lib().ce_set_attn_variant(prev)
@@ -303,7 +303,8 @@ def run_attn(qkv, B, L, H, causal):
 
 @pytest.mark.parametrize("B,L,H,causal", [(2, 577, 16, False), (3, 77, 12, True), (1, 1, 16, False),
                                           (2, 64, 4, False), (2, 65, 4, True), (1, 129, 2, False),
-                                          (1, 300, 12, True), (5, 577, 1, False)])
+                                          (1, 300, 12, True), (5, 577, 1, False), (1, 257, 2, False),
+                                          (2, 289, 3, False), (1, 97, 2, False)])
 def test_attention(B, L, H, causal, attn_var):
     g = torch.Generator(device="cpu").manual_seed(B * 1000 + L + H)
     qkv = (torch.randn(B * L, 3 * H * 64, generator=g) * 1.5).to(torch.bfloat16).to(DEV)
@@ -405,9 +406,10 @@ def test_layernorm(rows, D, bf16):
     assert err < (3e-2 if bf16 else 1e-4), err
 
 
+@pytest.mark.parametrize("var", [381, 1381])
 @pytest.mark.parametrize("s0", [6.0, -6.0, 0.0])
 @pytest.mark.parametrize("L", [577, 65, 129])
-def test_attention_cls_key_first(L, s0):
+def test_attention_cls_key_first(L, s0, var):
     """Variant 381 (key 0 folded in before the key tiles, tiles over keys 1..L-1) with key 0 dominant
     (s0 = +6: every query's score with it ~ +6 * 64 * 4 -> far past the fixed offset's +-64), far below
     (-6) and ordinary: vs f32 attention and vs the default variant."""
@@ -421,7 +423,7 @@ def test_attention_cls_key_first(L, s0):
             qkv[b * L, D:D + 64] = s0                                                        # key 0, head 0
     qkv = qkv.to(torch.bfloat16).to(DEV)
     ref = attn_ref(qkv, B, L, H, False)
-    prev = _lib.lib().ce_set_attn_variant(381)
+    prev = _lib.lib().ce_set_attn_variant(var)
     try:
         out = run_attn(qkv, B, L, H, False)
     finally:
