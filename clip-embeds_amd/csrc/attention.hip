@@ -77,18 +77,12 @@ __device__ __forceinline__ void barrier() {
 // L = 64k + 1, default), 125 (non-causal, other L), 88 (causal).  (Measured and removed in round 6:
 // MFMA row sums, a three-slot ring, early prologue loads, per-wave timelines and the persistent
 // variants)
-// QS (query sets per wave, round 6): 2 = each wave owns 64 queries as two 32-query MFMA sets that
-// share every K fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16) read: half the LDS
-// reads per MFMA and 256 queries per workgroup (L = 577: 3 workgroups per (b, h) instead of 5, so
-// 40 % fewer K/V tile transfers).  Two waves per SIMD at <= 256 registers instead of four at 128.
-// A wave whose second set lies wholly past L runs the one-set body (no MFMAs for padding).
-template <bool CAUSAL, int VAR, int QS = 1>
+template <bool CAUSAL, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qkv,
                                                     bf16_t* __restrict__ out, int Lp, int H,
                                                     float qscale, float* __restrict__ lse,
                                                     const int* __restrict__ seg) {
     static_assert((VAR & (8 | 16 | 64)) == (8 | 16 | 64) && (VAR & 3) <= 1, "attn_fwd: instantiated variant set");
-    static_assert(QS == 1 || (QS == 2 && !CAUSAL), "attn_fwd: two query sets per wave only without the causal mask");
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
     constexpr int MODE = VAR & 3;            // softmax: 0 general, 1 fixed offset
     constexpr bool ONEBAR = (VAR & 4) != 0;  // one barrier per key tile (next tile staged after it)
@@ -98,10 +92,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     // key tiles cover keys 1..L-1: L = 577 runs 9 full tiles instead of 9 + one single-key tile on the
     // masked general path
     constexpr bool CLSK = !CAUSAL && (VAR & 256) != 0;
-    constexpr int QB = QBLK * QS;            // queries per workgroup
     // XCD-aware bijective remap (as the GEMM): consecutive wgids = the q-blocks of one head, so
     // every workgroup that re-reads a head's K/V runs on the same XCD and shares its L2.
-    const int nqb = (Lp + QB - 1) / QB;
+    const int nqb = (Lp + QBLK - 1) / QBLK;
     const int nwg = gridDim.x;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
@@ -118,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     if (seg) {
         row0 = seg[b];
         L = seg[b + 1] - seg[b];
-        if (qb * QB >= L) return;
+        if (qb * QBLK >= L) return;
     }
     const bf16_t* base = qkv + (size_t)row0 * ld;
 
@@ -127,26 +120,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31;
     const int h2 = lane >> 5;
-    const int q_wave0 = qb * QB + wave * 32 * QS;     // first query of this wave (wave-uniform)
-    // query set j of the wave: queries q_wave0 + 32 j + (lane & 31)
-    int qrow[QS];
-#pragma unroll
-    for (int j = 0; j < QS; ++j) qrow[j] = q_wave0 + 32 * j + r;
+    const int qrow = qb * QBLK + wave * 32 + r;
+    const int q_wave0 = qb * QBLK + wave * 32;        // first query of this wave (wave-uniform)
 
     // Q fragments: B operand of S^T = K Q^T; lane holds Q[qrow][16ks + 8h2 .. +7]
-    bf16x8 qf[QS][4];
+    bf16x8 qf[4];
+    {
+        const bf16_t* qp = base + (size_t)min(qrow, L - 1) * ld + h * 64 + 8 * h2;
 #pragma unroll
-    for (int j = 0; j < QS; ++j) {
-        const bf16_t* qp = base + (size_t)min(qrow[j], L - 1) * ld + h * 64 + 8 * h2;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) qf[j][ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
         // scores in log2 units: q is pre-multiplied by log2(e)/sqrt(64), either here (qscale != 1,
         // the raw-qkv kernel entry) or already by the in_proj weights the engine uploads
         if (qscale != 1.0f) {
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) qf[j][ks][e] = (__bf16)((float)qf[j][ks][e] * qscale);
+                for (int e = 0; e < 8; ++e) qf[ks][e] = (__bf16)((float)qf[ks][e] * qscale);
         }
     }
 
@@ -156,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     const int kchunk = spos ^ ((tid >> 4) & 7);
     const int vchunk = spos ^ (((srow >> 1) & 1) << 2);   // V image swizzle (conflict-free tr reads)
     const int Lk = CLSK ? L - 1 : L;                     // keys covered by the tiles
-    const int kv_end = CAUSAL ? min(L, qb * QB + QB) : Lk;
+    const int kv_end = CAUSAL ? min(L, qb * QBLK + QBLK) : Lk;
     const int nkt = (kv_end + KBLK - 1) / KBLK;
     const bf16_t* kbase = base + D + h * 64 + (CLSK ? ld : 0);
     const bf16_t* vbase = base + 2 * D + h * 64 + (CLSK ? ld : 0);
@@ -206,6 +195,51 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
         const int chunk = dt * 4 + 2 * (G & 1) + (vp >> 1);
         voff[dt] = (4 * (G >> 1) + vq) * 128 + ((chunk ^ (((vq >> 1) & 1) << 2)) << 4) + (vp & 1) * 8;
     }
+
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+    float m_run = 0.f;   // running row max (log2 units); set exactly by the first tile
+    float l_run = 0.f;   // partial (this half's keys)
+    // wave-uniform: softmax offset fixed at 0 (MODE >= 1).  FAST0 (bit 32): tile 0 too starts on the
+    // fixed offset, its row sums checked from both sides (2^-64 <= sum <= 2^64: no row can underflow
+    // to l = 0 later); a row outside sends tile 0 to the general path, which sets the exact max
+    bool fast = MODE >= 1 && FAST0;
+    const f32x16 zero16 = {};
+    // CLSK: key 0's score (log2 units, both lane halves) and its term in O / l.  Offset 0 (the fixed
+    // offset) when every query of the wave has |s0| <= 64, else the exact s0 (general path)
+    float s0v = 0.f;
+    bool fix_ok = true;                      // wave-uniform: the offset may stay fixed at 0
+    if constexpr (CLSK) {
+        const bf16_t* k0 = base + D + h * 64 + 8 * h2;
+        float a = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
+            // (f32 FMAs: v_dot2_f32_bf16 here, with the packed multiplies below, took the kernel to 126
+            // VGPRs and four waves per SIMD, 1 % slower than three in a same-box A/B)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf((float)qf[ks][e], (float)kv[e], a);
+        }
+        s0v = a + __shfl_xor(a, 32, 64);
+        fix_ok = MODE >= 1 && __all(s0v <= 64.0f && s0v >= -64.0f);
+        float p0 = 1.0f;
+        if (fix_ok) p0 = __builtin_amdgcn_exp2f(s0v);
+        else { m_run = s0v; fast = false; }
+        if (h2 == 0) l_run = p0;
+        const bf16_t* v0 = base + 2 * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
+                o[dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
+                o[dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
+                o[dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
+                o[dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
+            }
+    }
+
     // O^T += V^T P^T with the V^T fragments read by inline asm (no wait on the LDS-DMA in flight):
     // the reads of 16-key group q + 1 are issued before the MFMAs of group q, counted lgkmcnt.
     // Addresses: one lane base per dt (smem + voff[dt]) plus compile-time immediates (VB = the V
@@ -213,77 +247,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     unsigned vaddr[2];
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) vaddr[dt] = (unsigned)(uintptr_t)(CE_LDS void*)(smem + voff[dt]);
-
-    // the loop and the epilogue for NS = 1 or 2 active query sets (wave-uniform: a wave's second set
-    // runs only when it holds a query below L)
-    auto body = [&](auto nsc) {
-        constexpr int NS = decltype(nsc)::value;
-        f32x16 o[NS][2];
-#pragma unroll
-        for (int j = 0; j < NS; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) { o[j][0][i] = 0.f; o[j][1][i] = 0.f; }
-        float m_run[NS];   // running row max (log2 units); set exactly by the first tile
-        float l_run[NS];   // partial (this half's keys)
-#pragma unroll
-        for (int j = 0; j < NS; ++j) { m_run[j] = 0.f; l_run[j] = 0.f; }
-        // wave-uniform: softmax offset fixed at 0 (MODE >= 1).  FAST0 (bit 32): tile 0 too starts on the
-        // fixed offset, its row sums checked from both sides (2^-64 <= sum <= 2^64: no row can underflow
-        // to l = 0 later); a row outside sends tile 0 to the general path, which sets the exact max
-        bool fast = MODE >= 1 && FAST0;
-        const f32x16 zero16 = {};
-        // CLSK: key 0's score (log2 units, both lane halves) and its term in O / l.  Offset 0 (the fixed
-        // offset) when every query of the wave has |s0| <= 64, else the exact s0 (general path)
-        float s0v[NS];
-        bool fix_ok = true;                      // wave-uniform: the offset may stay fixed at 0
-#pragma unroll
-        for (int j = 0; j < NS; ++j) s0v[j] = 0.f;
-        if constexpr (CLSK) {
-            const bf16_t* k0 = base + D + h * 64 + 8 * h2;
-            float a[NS];
-#pragma unroll
-            for (int j = 0; j < NS; ++j) a[j] = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k0 + 16 * ks);
-                // (f32 FMAs: v_dot2_f32_bf16 here, with the packed multiplies below, took the kernel to 126
-                // VGPRs and four waves per SIMD, 1 % slower than three in a same-box A/B)
-#pragma unroll
-                for (int j = 0; j < NS; ++j)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) a[j] = fmaf((float)qf[j][ks][e], (float)kv[e], a[j]);
-            }
-            bool in_range = true;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                s0v[j] = a[j] + __shfl_xor(a[j], 32, 64);
-                in_range = in_range && s0v[j] <= 64.0f && s0v[j] >= -64.0f;
-            }
-            fix_ok = MODE >= 1 && __all(in_range);
-            const bf16_t* v0 = base + 2 * D + h * 64;
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                float p0 = 1.0f;
-                if (fix_ok) p0 = __builtin_amdgcn_exp2f(s0v[j]);
-                else { m_run[j] = s0v[j]; fast = false; }
-                if (h2 == 0) l_run[j] = p0;
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const uint2 w = *reinterpret_cast<const uint2*>(v0 + dt * 32 + 8 * g + 4 * h2);
-                        o[j][dt][4 * g + 0] = p0 * __uint_as_float(w.x << 16);
-                        o[j][dt][4 * g + 1] = p0 * __uint_as_float(w.x & 0xffff0000u);
-                        o[j][dt][4 * g + 2] = p0 * __uint_as_float(w.y << 16);
-                        o[j][dt][4 * g + 3] = p0 * __uint_as_float(w.y & 0xffff0000u);
-                    }
-            }
-        }
-
-        auto pv_asm = [&](auto vbc, const bf16x8 (&pf)[NS][2][2], bool with_half2) {
-            constexpr int VB = decltype(vbc)::value;
-            typedef __attribute__((ext_vector_type(8))) short s16x8;
-            s16x4 vr[2][2][2];        // [ring][dt][lo, hi]
+    auto pv_asm = [&](auto vbc, const bf16x8 (&pf)[2][2], bool with_half2) {
+        constexpr int VB = decltype(vbc)::value;
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x4 vr[2][2][2];        // [ring][dt][lo, hi]
 #define CE_TRV(R, DT, H, OFF) \
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[R][DT][H]) : "v"(vaddr[DT]), "n"(OFF))
 #define CE_ISSUE(Q) \
@@ -291,253 +258,213 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const bf16_t* __restrict__ qk
     CE_TRV((Q) & 1, 0, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024); \
     CE_TRV((Q) & 1, 1, 0, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128); \
     CE_TRV((Q) & 1, 1, 1, VB + (((Q) >> 1) * 32 + 16 * ((Q) & 1)) * 128 + 1024)
-            auto mf = [&](int q) {
+        auto mf = [&](int q) {
 #pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-                    for (int j = 0; j < NS; ++j)
-                        o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8),
-                                                                           pf[j][q >> 1][q & 1], o[j][dt], 0, 0, 0);
-                }
-            };
-            // one 16-key group at a time (issuing the next group ahead holds 16 more VGPRs: 156 > 128,
-            // three waves per SIMD instead of four); the other waves on the SIMD cover the LDS latency
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (q >= 2 && !with_half2) break;
-                if (q == 0) { CE_ISSUE(0); }
-                else if (q == 1) { CE_ISSUE(1); }
-                else if (q == 2) { CE_ISSUE(2); }
-                else { CE_ISSUE(3); }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                mf(q);
+            for (int dt = 0; dt < 2; ++dt) {
+                const s16x8 v8 = __builtin_shufflevector(vr[q & 1][dt][0], vr[q & 1][dt][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf[q >> 1][q & 1],
+                                                               o[dt], 0, 0, 0);
             }
+        };
+        // one 16-key group at a time (issuing the next group ahead holds 16 more VGPRs: 156 > 128,
+        // three waves per SIMD instead of four); the other waves on the SIMD cover the LDS latency
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q >= 2 && !with_half2) break;
+            if (q == 0) { CE_ISSUE(0); }
+            else if (q == 1) { CE_ISSUE(1); }
+            else if (q == 2) { CE_ISSUE(2); }
+            else { CE_ISSUE(3); }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            mf(q);
+        }
 #undef CE_ISSUE
 #undef CE_TRV
-        };
+    };
 
-        // rescale of O and l of set j by 2^-delta (delta per lane, equal on lanes l and l^32)
-        auto rescale = [&](int j, float delta) {
-            const float alpha = __builtin_amdgcn_exp2f(-delta);
-            l_run[j] *= alpha;
+    // rescale of O and l by 2^-delta (delta per lane, equal on lanes l and l^32)
+    auto rescale = [&](float delta) {
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        l_run *= alpha;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) { o[j][0][i] *= alpha; o[j][1][i] *= alpha; }
-            m_run[j] += delta;
-        };
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        m_run += delta;
+    };
 
-        stage(0, 0);
-        // one key tile; BUF (the ring slot, t & 1) is a compile-time constant so every LDS address is a
-        // per-lane offset plus an immediate (the loop is unrolled by two)
-        auto tile = [&](const int t, auto bufc) {
-            constexpr int BUF = decltype(bufc)::value;
-            if (ONEBAR) {
-                // tile t landed (the only DMA in flight) and every wave is done with tile t-1, whose
-                // slot BUF^1 then takes tile t+1
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                barrier();
-                if (t + 1 < nkt) stage(t + 1, BUF ^ 1);
+    stage(0, 0);
+    // one key tile; BUF (the ring slot, t & 1) is a compile-time constant so every LDS address is a
+    // per-lane offset plus an immediate (the loop is unrolled by two)
+    auto tile = [&](const int t, auto bufc) {
+        constexpr int BUF = decltype(bufc)::value;
+        if (ONEBAR) {
+            // tile t landed (the only DMA in flight) and every wave is done with tile t-1, whose
+            // slot BUF^1 then takes tile t+1
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            barrier();
+            if (t + 1 < nkt) stage(t + 1, BUF ^ 1);
+        } else {
+            if (t + 1 < nkt) {
+                stage(t + 1, BUF ^ 1);
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             } else {
-                if (t + 1 < nkt) {
-                    stage(t + 1, BUF ^ 1);
-                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                barrier();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            const char* kb = smem + BUF * STAGE_BYTES;
-
-            // waves whose queries are all padding, or (causal) whose queries all precede this key
-            // tile, skip the math but keep the workgroup barriers
-            const bool active = q_wave0 < L && !(CAUSAL && t * KBLK > q_wave0 + 31);
-            // second 32-key subtile entirely past the sequence end (L = 577: the last tile holds one
-            // key) or (causal) entirely above this wave's diagonal: skip its MFMAs and exponentials
-            const bool half2 = (t * KBLK + 32 < Lk) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
-            const int key0 = t * KBLK;
-            // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
-            const bool need_mask = (key0 + KBLK > Lk) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
-            const bool fast_tile = MODE >= 1 && fast && half2 && !need_mask;   // wave-uniform
-            bool redo = false;
-            if (active && fast_tile) {
-                // ---- fixed-offset tile: S^T = K Q^T from a zero accumulator, p = exp2(s) ----
-                f32x16 s[NS][2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) {
-                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
-#pragma unroll
-                        for (int j = 0; j < NS; ++j)
-                            s[j][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][ks], ks == 0 ? zero16 : s[j][kt2],
-                                                                                0, 0, 0);
-                    }
-                float psum[NS];
-                bf16x8 pf[NS][2][2];
-                bool bad = false;
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) {
-                                const float pv_ = __builtin_amdgcn_exp2f(s[j][kt2][8 * s2 + e]);
-                                ps[e & 3] += pv_;
-                                pf[j][kt2][s2][e] = (__bf16)pv_;
-                            }
-                    psum[j] = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-                    // (!(x <= 2^64) also catches NaN)
-                    bad = bad || !(psum[j] <= 0x1p64f) || (FAST0 && t == 0 && !(psum[j] >= 0x1p-64f));
-                }
-                if (!__any(bad)) {
-#pragma unroll
-                    for (int j = 0; j < NS; ++j) l_run[j] += psum[j];
-                    __builtin_amdgcn_sched_barrier(0);
-                    pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, true);
-                } else {
-                    // rare: the tile is redone on the general path below (exact row max, rescale),
-                    // and the wave stays there
-                    fast = false;
-                    redo = true;
-                }
-            }
-            if (active && (redo || !(MODE >= 1 && fast_tile))) {
-                // ---- S^T = K Q^T (two 32-key subtiles) ----
-                f32x16 s[NS][2];
-#pragma unroll
-                for (int kt2 = 0; kt2 < 2; ++kt2) {
-#pragma unroll
-                    for (int j = 0; j < NS; ++j)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) s[j][kt2][i] = kt2 == 1 && !half2 ? -INFINITY : -m_run[j];
-                    if (kt2 == 1 && !half2) continue;
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) {
-                        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
-#pragma unroll
-                        for (int j = 0; j < NS; ++j)
-                            s[j][kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][ks], s[j][kt2], 0, 0, 0);
-                    }
-                }
-
-                // ---- online softmax, log2 domain.  The S accumulator starts at -m_run, so the MFMA
-                // leaves s = q.k - m_run (q pre-scaled): p = exp2(s) needs no per-score FMA ----
-                if (need_mask) {
-#pragma unroll
-                    for (int j = 0; j < NS; ++j)
-#pragma unroll
-                        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                            for (int i = 0; i < 16; ++i) {
-                                const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
-                                const bool masked = (key >= Lk) || (CAUSAL && key > qrow[j]);
-                                s[j][kt2][i] = masked ? -INFINITY : s[j][kt2][i];
-                            }
-                }
-                float tmax[NS];
-                bool in_range = true;
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    tmax[j] = s[j][0][0];
-#pragma unroll
-                    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                        for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax[j] = fmaxf(tmax[j], s[j][kt2][i]);
-                    tmax[j] = fmaxf(tmax[j], __shfl_xor(tmax[j], 32, 64));    // relative to m_run
-                    in_range = in_range && tmax[j] <= 64.0f && tmax[j] >= -64.0f;
-                }
-                // Deferred rescale (guide T13): m_run moves on the first tile (to the exact row max:
-                // key 0 is never masked, so it is finite) and afterwards only when a row max exceeds
-                // it by more than the threshold (8, or 64 with the offset fixed at 0), so p stays far
-                // from the f32 / bf16 overflow and O / l are rarely rescaled.  O and l always see the
-                // same factor, and the decision precedes this tile's P, so no P.V product straddles it.
-                // VARs >= 1: when tile 0's row maxima all lie within +-64, the offset stays 0.
-                // (CLSK: O / l already hold key 0's term, so the first move rescales them, and the exact
-                // max includes key 0; the fixed offset needs key 0 on it too)
-                const bool fix0 = MODE >= 1 && t == 0 && fix_ok && __all(in_range);
-                if (fix0) fast = true;
-                const float thr = fast ? 64.0f : 8.0f;
-                bool moved = false;
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    if (!fix0 && (t == 0 || __any(tmax[j] > thr))) {
-                        const float delta = t == 0 ? (CLSK ? fmaxf(tmax[j], s0v[j] - m_run[j]) : tmax[j])
-                                                   : fmaxf(tmax[j], 0.f);
-                        if (t != 0 || CLSK) rescale(j, delta);
-                        else m_run[j] += delta;
-                        moved = true;
-#pragma unroll
-                        for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                            for (int i = 0; i < 16; ++i) s[j][kt2][i] -= delta;
-                    }
-                }
-                if (moved) fast = false;
-                bf16x8 pf[NS][2][2];
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    float psum = 0.f;
-#pragma unroll
-                    for (int kt2 = 0; kt2 < 2; ++kt2)
-#pragma unroll
-                        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) {
-                                if (kt2 == 1 && !half2) { pf[j][kt2][s2][e] = (__bf16)0.f; continue; }
-                                const float pv_ = __builtin_amdgcn_exp2f(s[j][kt2][8 * s2 + e]);
-                                psum += pv_;
-                                pf[j][kt2][s2][e] = (__bf16)pv_;
-                            }
-                    l_run[j] += psum;
-                }
-                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, half2);
-            }
-            if (!ONEBAR) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                barrier();
-            }
-        };
-        for (int t = 0; t < nkt; t += 2) {
-            tile(t, std::integral_constant<int, 0>{});
-            if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
+            barrier();
         }
+        const char* kb = smem + BUF * STAGE_BYTES;
+        const char* vb = kb + TILE_KV_BYTES;
 
-        // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
+        // waves whose queries are all padding, or (causal) whose queries all precede this key
+        // tile, skip the math but keep the workgroup barriers
+        const bool active = q_wave0 < L && !(CAUSAL && t * KBLK > q_wave0 + 31);
+        // second 32-key subtile entirely past the sequence end (L = 577: the last tile holds one
+        // key) or (causal) entirely above this wave's diagonal: skip its MFMAs and exponentials
+        const bool half2 = (t * KBLK + 32 < Lk) && !(CAUSAL && t * KBLK + 32 > q_wave0 + 31);
+        const int key0 = t * KBLK;
+        // masking only on the ragged last tile and (causal) on tiles that cross the diagonal
+        const bool need_mask = (key0 + KBLK > Lk) || (CAUSAL && key0 + KBLK - 1 > q_wave0);
+        const bool fast_tile = MODE >= 1 && fast && half2 && !need_mask;   // wave-uniform
+        bool redo = false;
+        if (active && fast_tile) {
+            // ---- fixed-offset tile: S^T = K Q^T from a zero accumulator, p = exp2(s) ----
+            f32x16 s[2];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
-            const float l_tot = l_run[j] + __shfl_xor(l_run[j], 32, 64);
-            const float inv = 1.0f / l_tot;
-            // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
-            if (lse && qrow[j] < L && h2 == 0) lse[((size_t)b * H + h) * Lp + qrow[j]] = m_run[j] + __log2f(l_tot);
-            bf16_t* op = out + ((size_t)row0 + min(qrow[j], L - 1)) * D + h * 64;
-            // 16-B stores: lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
-            // trades the lower lane's odd-g words for the upper lane's even-g words, so each lane
-            // stores 8 consecutive d (16 B): the lower lane d = 16gp + 0..7, the upper 16gp + 8..15
+            for (int kt2 = 0; kt2 < 2; ++kt2)
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                for (int gp = 0; gp < 2; ++gp) {
-                    const int g0 = 2 * gp, g1 = 2 * gp + 1;
-                    const uint32_t ax = pack_bf2(o[j][dt][4 * g0 + 0] * inv, o[j][dt][4 * g0 + 1] * inv);
-                    const uint32_t ay = pack_bf2(o[j][dt][4 * g0 + 2] * inv, o[j][dt][4 * g0 + 3] * inv);
-                    const uint32_t bx = pack_bf2(o[j][dt][4 * g1 + 0] * inv, o[j][dt][4 * g1 + 1] * inv);
-                    const uint32_t by = pack_bf2(o[j][dt][4 * g1 + 2] * inv, o[j][dt][4 * g1 + 3] * inv);
-                    const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-                    const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-                    if (qrow[j] < L)
-                        *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
+                for (int ks = 0; ks < 4; ++ks) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                    s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], ks == 0 ? zero16 : s[kt2], 0, 0, 0);
                 }
+            float ps[4] = {0.f, 0.f, 0.f, 0.f};
+            bf16x8 pf[2][2];
+#pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                        ps[j & 3] += pv_;
+                        pf[kt2][s2][j] = (__bf16)pv_;
+                    }
+            const float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+            // (!(x <= 2^64) also catches NaN)
+            const bool overflow = __any(!(psum <= 0x1p64f)) || (FAST0 && t == 0 && __any(!(psum >= 0x1p-64f)));
+            if (!overflow) {
+                l_run += psum;
+                __builtin_amdgcn_sched_barrier(0);
+                pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, true);
+            } else {
+                // rare: the tile is redone on the general path below (exact row max, rescale),
+                // and the wave stays there
+                fast = false;
+                redo = true;
+            }
+        }
+        if (active && (redo || !(MODE >= 1 && fast_tile))) {
+            // ---- S^T = K Q^T (two 32-key subtiles) ----
+            f32x16 s[2];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2) {
+    #pragma unroll
+                for (int i = 0; i < 16; ++i) s[kt2][i] = kt2 == 1 && !half2 ? -INFINITY : -m_run;
+                if (kt2 == 1 && !half2) continue;
+    #pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + koff[kt2][ks]);
+                    s[kt2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt2], 0, 0, 0);
+                }
+            }
+
+            // ---- online softmax, log2 domain.  The S accumulator starts at -m_run, so the MFMA
+            // leaves s = q.k - m_run (q pre-scaled): p = exp2(s) needs no per-score FMA ----
+            if (need_mask) {
+    #pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int key = key0 + kt2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * h2;
+                        const bool masked = (key >= Lk) || (CAUSAL && key > qrow);
+                        s[kt2][i] = masked ? -INFINITY : s[kt2][i];
+                    }
+            }
+            float tmax = s[0][0];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                for (int i = (kt2 == 0 ? 1 : 0); i < 16; ++i) tmax = fmaxf(tmax, s[kt2][i]);
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));    // relative to m_run
+            // Deferred rescale (guide T13): m_run moves on the first tile (to the exact row max:
+            // key 0 is never masked, so it is finite) and afterwards only when a row max exceeds
+            // it by more than the threshold (8, or 64 with the offset fixed at 0), so p stays far
+            // from the f32 / bf16 overflow and O / l are rarely rescaled.  O and l always see the
+            // same factor, and the decision precedes this tile's P, so no P.V product straddles it.
+            // VARs >= 1: when tile 0's row maxima all lie within +-64, the offset stays 0.
+            // (CLSK: O / l already hold key 0's term, so the first move rescales them, and the exact
+            // max includes key 0; the fixed offset needs key 0 on it too)
+            const bool fix0 = MODE >= 1 && t == 0 && fix_ok && __all(tmax <= 64.0f && tmax >= -64.0f);
+            if (fix0) fast = true;
+            if (!fix0 && (t == 0 || __any(tmax > (fast ? 64.0f : 8.0f)))) {
+                const float delta = t == 0 ? (CLSK ? fmaxf(tmax, s0v - m_run) : tmax) : fmaxf(tmax, 0.f);
+                if (t != 0 || CLSK) rescale(delta);
+                else m_run += delta;
+                fast = false;
+    #pragma unroll
+                for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) s[kt2][i] -= delta;
+            }
+            float psum = 0.f;
+            bf16x8 pf[2][2];
+    #pragma unroll
+            for (int kt2 = 0; kt2 < 2; ++kt2)
+    #pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (kt2 == 1 && !half2) { pf[kt2][s2][j] = (__bf16)0.f; continue; }
+                        const float pv_ = __builtin_amdgcn_exp2f(s[kt2][8 * s2 + j]);
+                        psum += pv_;
+                        pf[kt2][s2][j] = (__bf16)pv_;
+                    }
+            l_run += psum;
+            pv_asm(std::integral_constant<int, BUF * STAGE_BYTES + TILE_KV_BYTES>{}, pf, half2);
+        }
+        if (!ONEBAR) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            barrier();
         }
     };
-    if constexpr (QS == 2) {
-        if (q_wave0 + 32 < L) body(std::integral_constant<int, 2>{});
-        else body(std::integral_constant<int, 1>{});
-    } else {
-        body(std::integral_constant<int, 1>{});
+    for (int t = 0; t < nkt; t += 2) {
+        tile(t, std::integral_constant<int, 0>{});
+        if (t + 1 < nkt) tile(t + 1, std::integral_constant<int, 1>{});
+    }
+
+    // ---- epilogue: O = O^T / l, lane holds query qrow, d = dt*32 + 8g + 4h2 + (0..3) ----
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.0f / l_tot;
+    // training: log2-domain log-sum-exp of the row (P = exp2(S - lse) in the attention backward)
+    if (lse && qrow < L && h2 == 0) lse[((size_t)b * H + h) * Lp + qrow] = m_run + __log2f(l_tot);
+    bf16_t* op = out + ((size_t)row0 + min(qrow, L - 1)) * D + h * 64;
+    {
+        // 16-B stores: lane h2 = 0 holds d = 8g + 0..3 and its partner l^32 d = 8g + 4..7: v_permlane32_swap
+        // trades the lower lane's odd-g words for the upper lane's even-g words, so each lane
+        // stores 8 consecutive d (16 B): the lower lane d = 16gp + 0..7, the upper 16gp + 8..15
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp) {
+                const int g0 = 2 * gp, g1 = 2 * gp + 1;
+                const uint32_t ax = pack_bf2(o[dt][4 * g0 + 0] * inv, o[dt][4 * g0 + 1] * inv);
+                const uint32_t ay = pack_bf2(o[dt][4 * g0 + 2] * inv, o[dt][4 * g0 + 3] * inv);
+                const uint32_t bx = pack_bf2(o[dt][4 * g1 + 0] * inv, o[dt][4 * g1 + 1] * inv);
+                const uint32_t by = pack_bf2(o[dt][4 * g1 + 2] * inv, o[dt][4 * g1 + 3] * inv);
+                const auto x = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                const auto y = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                if (qrow < L)
+                    *reinterpret_cast<uint4*>(op + dt * 32 + 16 * gp + 8 * h2) = make_uint4(x[0], y[0], x[1], y[1]);
+            }
     }
 }
 
@@ -685,35 +612,26 @@ hipError_t launch_attention_rows(const bf16_t* qkv, const int* qrows, bf16_t* ou
 hipError_t launch_attention(const bf16_t* qkv, bf16_t* out, int B, int L, int H, bool causal, bool q_prescaled,
                             hipStream_t s, float* lse, const int* seg) {
     if (B <= 0 || L <= 0) return hipSuccess;
+    const dim3 grid((unsigned)(((L + QBLK - 1) / QBLK) * H * B));
     const float qscale = q_prescaled ? 1.0f : kAttnQScale;
-    const int v = g_attn_var.load(std::memory_order_acquire);
-    // two query sets per wave (v >= 1000): 256 queries per workgroup
-    const int qs = (!causal && v >= 1000) ? 2 : 1;
-    const dim3 grid((unsigned)(((L + QBLK * qs - 1) / (QBLK * qs)) * H * B));
-#define CE_ATTN_LAUNCH(C, V, QS) \
-    hipLaunchKernelGGL((attn_fwd<C, V, QS>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
-    // key 0 first (CLSK) needs the keys after the first to fill whole tiles
-    const bool clsk = (v % 1000) == 381 && (L - 1) % KBLK == 0 && L > 1;
+#define CE_ATTN_LAUNCH(C, V) hipLaunchKernelGGL((attn_fwd<C, V>), grid, dim3(256), 0, s, qkv, out, L, H, qscale, lse, seg)
     // the text tower's causal tiles all cross the diagonal or the ragged end: general softmax
+    const int v = g_attn_var.load(std::memory_order_acquire);
     if (causal) {
-        CE_ATTN_LAUNCH(true, 88, 1);
-    } else if (qs == 2) {
-        if (clsk) CE_ATTN_LAUNCH(false, 381, 2);
-        else CE_ATTN_LAUNCH(false, 125, 2);
-    } else if (clsk) {
-        CE_ATTN_LAUNCH(false, 381, 1);
+        CE_ATTN_LAUNCH(true, 88);
+    } else if (v == 381 && (L - 1) % KBLK == 0 && L > 1) {
+        // key 0 first (CLSK) needs the keys after the first to fill whole tiles
+        CE_ATTN_LAUNCH(false, 381);
     } else {
-        CE_ATTN_LAUNCH(false, 125, 1);
+        CE_ATTN_LAUNCH(false, 125);
     }
 #undef CE_ATTN_LAUNCH
     return hipGetLastError();
 }
 
 int set_attn_variant(int var) {
-    // 381: key 0 ahead of the key tiles where (L - 1) % 64 == 0 (default); 125: the key tiles only;
-    // + 1000 (1381, 1125): two 32-query sets per wave (non-causal)
-    const int v = (var == 125 || var == 1125 || var == 1381) ? var : 381;
-    return g_attn_var.exchange(v);
+    // 381: key 0 ahead of the key tiles where (L - 1) % 64 == 0 (default); 125: the key tiles only
+    return g_attn_var.exchange(var == 125 ? 125 : 381);
 }
 
 }  // namespace ce
