@@ -240,3 +240,51 @@ def test_two_ranks_equal_one_rank_on_concatenated_batch():
         np.testing.assert_array_equal(got[r]["upd"], got[0]["upd"])
         big = np.abs(g1) > 0.1 * np.abs(g1).max()
         np.testing.assert_allclose(got[r]["upd"][big], u1[big], rtol=2e-3, atol=1e-9)
+
+
+@pytest.mark.parametrize("B", [1, 5])
+def test_small_batches_vs_oracle(cfg, sd, B):
+    """B = 1 (the global term's 1 x 1 logits: zero loss and gradient) and an odd batch, sparc without
+    RoPE on the caption path, vs the f32 autograd restatement."""
+    from oracle.sparc_train_torch import TorchSparcTrainStep
+    m = _model(sparc, cfg, sd)
+    tr = clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0)
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1700 + B)).cuda()
+    caps = torch.from_numpy(W.synthetic_captions(B, seed=2700 + B)).cuda()
+    loss = float(tr.compute_grads(imgs, caps))
+    _, pt = m.clip_model.encode_image(imgs)
+    _, tt = m.clip_model.encode_text(caps)
+    mask = (torch.arange(77, device="cuda")[None, :] <= caps.argmax(-1)[:, None]).float()
+    step = TorchSparcTrainStep({n: v.detach() for n, v in tr.views.items()}, device="cuda")
+    ref_loss, ref_grads, _ = step.loss_and_grads(pt, mask, text_tokens=tt, p=0.0)
+    _vs_oracle(tr, ref_loss, ref_grads, loss)
+
+
+def test_errors(cfg, sd):
+    """The C ABI's state machine and argument checks (include/clipembed.h: ce_sparc_train_*)."""
+    from clipembed import _lib
+    from clipembed.model import _ptr, _stream
+    m = _model(sparc_rope, cfg, sd)
+    tr = clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0)
+    h, s = tr.e.h, _stream(tr.dev)
+    with pytest.raises(RuntimeError, match="needs ce_sparc_train_forward"):
+        _lib.call("ce_sparc_train_backward", h, s)
+    x = torch.zeros(2, 576, 1024, device="cuda")
+    t = torch.zeros(2, 81, 768, device="cuda")
+    with pytest.raises(RuntimeError, match="no ce_sparc_train_forward"):
+        _lib.call("ce_sparc_train_loss_grad", h, s, _ptr(x), _ptr(x), 2, 0, _ptr(x), 1.0, 0.1, 0.5, 1.0, _ptr(x))
+    import ctypes
+    fwd = lambda P, rope, T, p: _lib.call("ce_sparc_train_forward", h, s, _ptr(x), 2, P, rope, _ptr(t), 0, T, 1 / 576, p,
+                                          ctypes.c_uint64(0), None, None, None)
+    with pytest.raises(RuntimeError, match="T <= 80"):
+        fwd(576, 1, 81, 0.0)
+    with pytest.raises(RuntimeError, match="rope tables"):
+        fwd(500, 1, 77, 0.0)
+    with pytest.raises(RuntimeError, match="dropout"):
+        fwd(576, 1, 77, 1.0)
+    # a bind that leaves a head tensor out
+    Pn = (_lib.Tensor * 1)()
+    from clipembed.train import _tensor_entry
+    Pn[0] = _tensor_entry(b"visual_projection.0.weight", tr.views["visual_projection.0.weight"])
+    with pytest.raises(RuntimeError, match="not bound"):
+        _lib.call("ce_sparc_train_bind", h, Pn, Pn, 1)
