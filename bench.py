@@ -139,7 +139,7 @@ def load_mfma_busy(tag):
     """Counter-based MFMA utilisation of `tag` (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE, one rocprofv3
     --pmc pass over this bench; tools/summarize_mfma.py -> profiles/<round>/mfma_busy.json, the latest
     round that has one), if measured."""
-    for rnd in ("r05", "r04"):
+    for rnd in ("r06", "r05", "r04"):
         path = os.path.join(REPO, "profiles", rnd, "mfma_busy.json")
         try:
             with open(path) as f:
