@@ -132,7 +132,8 @@ _SIGNATURES = {
     "ce_sparc_train_bind": (c_int, [c_void_p, POINTER(Tensor), POINTER(Tensor), c_int]),
     "ce_sparc_train_sync_weights": (c_int, [c_void_p, c_void_p]),
     "ce_sparc_train_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int,
-                                       c_float, c_float, ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
+                                       c_float, c_float, ctypes.c_uint64, ctypes.c_int64, c_void_p, c_void_p,
+                                       c_void_p]),
     "ce_sparc_train_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_float,
                                          c_float, c_float, c_float, c_void_p]),
     "ce_sparc_train_backward": (c_int, [c_void_p, c_void_p]),

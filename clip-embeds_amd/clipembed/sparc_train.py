@@ -19,7 +19,9 @@ torch.optim.Adam(lr=1e-4)):
   5. Adam (ce_adamw with weight decay 0 is torch.optim.Adam) on the f32 masters, then the engine's
      compute copies of the heads are refreshed (ce_sparc_train_sync_weights).
 
-Dropout masks come from a counter hash of (seed + step) (ce_sparc_train_forward), not torch's RNG.
+Dropout masks come from a counter hash of (seed + step) over each element's index in the GLOBAL batch
+(ce_sparc_train_forward's sample0 = this rank's first sample), not torch's RNG: N ranks draw the masks
+of the single-device step on the concatenated batch.
 """
 from __future__ import annotations
 
@@ -113,12 +115,19 @@ class SparcHeadTrainer:
         B, P, _ = patch_tokens.shape
         T = text.shape[1]
         Pd = m.clip_model.cfg.pacl_dim
+        sample0 = 0
+        if self.world > 1:                     # this rank's first sample in the global batch
+            n = torch.tensor([B], device=self.dev, dtype=torch.int64)
+            sizes = [torch.empty_like(n) for _ in range(self.world)]
+            dist.all_gather(sizes, n)
+            sample0 = int(sum(int(x) for x in sizes[:self.rank]))
         v = torch.empty(B, P, Pd, device=self.dev, dtype=torch.float32)
         l = torch.empty(B, T, Pd, device=self.dev, dtype=torch.float32)
         g = torch.empty(B, T, Pd, device=self.dev, dtype=torch.float32)
         self.last_seed = self.seed + self.step_count
         _lib.call("ce_sparc_train_forward", self.e.h, _stream(self.dev), _ptr(patch_tokens), B, P, m.rope, _ptr(text),
-                  mode, T, float(m.sigma), float(self.dropout), ctypes.c_uint64(self.last_seed), _ptr(v), _ptr(l), _ptr(g))
+                  mode, T, float(m.sigma), float(self.dropout), ctypes.c_uint64(self.last_seed), ctypes.c_int64(sample0),
+                  _ptr(v), _ptr(l), _ptr(g))
         self._caps = caps
         return v, l, g
 

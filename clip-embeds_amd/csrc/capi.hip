@@ -187,6 +187,7 @@ struct ce_handle {
     int sp_B = 0, sp_P = 0, sp_T = 0, sp_text = 0, sp_state = 0;   // state: 1 forward done, 2 loss grad done
     float sp_sigma = 0.f, sp_drop = 0.f;
     uint64_t sp_seed = 0;
+    int64_t sp_sample0 = 0;
     std::vector<KStat> stats;
     std::map<std::string, int> stat_idx;
     std::vector<Pending> pending;
@@ -2222,7 +2223,7 @@ int ce_sparc_train_sync_weights(ce_handle* h, void* stream) {
 
 int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens, int B, int P, int rope,
                            const float* text, int text_mode, int T, float sigma, float dropout, uint64_t seed,
-                           float* out_v, float* out_l, float* out_g) {
+                           int64_t sample0, float* out_v, float* out_l, float* out_g) {
     if (!h || !patch_tokens || !text) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: null argument");
     if (h->sp_bound.empty()) return fail(CE_ERR_STATE, "ce_sparc_train_forward: no head bound (ce_sparc_train_bind)");
     if (B <= 0 || P <= 0 || T <= 0 || T > 80) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: bad sizes (T <= 80)");
@@ -2231,6 +2232,7 @@ int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens
         return fail(CE_ERR_INVALID, "ce_sparc_train_forward: rope tables cover %d patches", h->G * h->G);
     if (text_mode != 0 && text_mode != 1) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: text_mode 0 or 1");
     if (!(dropout >= 0.f && dropout < 1.f)) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: dropout in [0, 1)");
+    if (sample0 < 0) return fail(CE_ERR_INVALID, "ce_sparc_train_forward: sample0 < 0");
     CE_TRY(check_ready(h, true));
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
@@ -2245,7 +2247,7 @@ int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens
     else HIP_TRY(hipMemcpyAsync(w.xv, patch_tokens, (size_t)w.N1 * Dv * 4, hipMemcpyDeviceToDevice, s));
     CE_TRY(timed(h, s, "sparc_ln_v", 0.0, 6.0 * w.N1 * Dv, [&] {
         return ce::launch_ln_drop(w.xv, W(h, "visual_projection.0.weight"), W(h, "visual_projection.0.bias"), w.N1, Dv,
-                                  dropout, 2 * seed, w.hv, true, w.stv, s); }));
+                                  dropout, 2 * seed, (long)sample0 * P, w.hv, true, w.stv, s); }));
     CE_TRY(tgemm(h, s, "sparc_head_v", w.hv, Dv, W<bf16_t>(h, "visual_projection.2.linear_projection.0.weight"), Dv, N1,
                  Pd, Dv, W(h, "visual_projection.2.linear_projection.0.bias"), ce::ACT_NONE_, nullptr, w.ylin, false, w.gpart));
     {
@@ -2264,7 +2266,7 @@ int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens
         HIP_TRY(hipMemcpyAsync(w.xt, text, (size_t)w.Nt * E * 4, hipMemcpyDeviceToDevice, s));
         CE_TRY(timed(h, s, "sparc_ln_t", 0.0, 8.0 * w.Nt * E, [&] {
             return ce::launch_ln_drop(w.xt, W(h, "text_projection.0.weight"), W(h, "text_projection.0.bias"), w.Nt, E,
-                                      dropout, 2 * seed + 1, w.ht, false, w.stt, s); }));
+                                      dropout, 2 * seed + 1, (long)sample0 * T, w.ht, false, w.stt, s); }));
         CE_TRY(sparc_fgemm(h, s, "sparc_head_t", w.ht, E, 0, sp_param(h, "text_projection.2.weight"), E, 0, w.l, Pd, 0,
                            (int)w.Nt, Pd, E, 1, 1.f, true, W(h, "text_projection.2.bias")));
     } else {
@@ -2283,7 +2285,7 @@ int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens
     if (out_l) HIP_TRY(hipMemcpyAsync(out_l, w.Ln, (size_t)w.Nt * Pd * 4, hipMemcpyDeviceToDevice, s));
     if (out_g) HIP_TRY(hipMemcpyAsync(out_g, w.Gn, (size_t)B * T * Pd * 4, hipMemcpyDeviceToDevice, s));
     h->sp_B = B; h->sp_P = P; h->sp_T = T; h->sp_text = text_mode;
-    h->sp_sigma = sigma; h->sp_drop = dropout; h->sp_seed = seed;
+    h->sp_sigma = sigma; h->sp_drop = dropout; h->sp_seed = seed; h->sp_sample0 = sample0;
     h->sp_state = 1;
     return CE_OK;
 }
@@ -2390,7 +2392,8 @@ int ce_sparc_train_backward(ce_handle* h, void* stream) {
                            Pd, E, Nt, 1, 1.f, false));
         CE_TRY(sparc_fgemm(h, s, "sparc_bwd_head_t", w.dl, Pd, 0, sp_param(h, "text_projection.2.weight"), E, 0, w.dht, E, 0,
                            Nt, E, Pd, 1, 1.f, false));
-        CE_TRY(check_launch(ce::launch_ln_grad(w.dht, w.xt, w.stt, Nt, E, p, 2 * seed + 1, sp_grad(h, "text_projection.0.weight"),
+        CE_TRY(check_launch(ce::launch_ln_grad(w.dht, w.xt, w.stt, Nt, E, p, 2 * seed + 1, (long)h->sp_sample0 * T,
+                                               sp_grad(h, "text_projection.0.weight"),
                                                sp_grad(h, "text_projection.0.bias"), w.lng, s), "sparc ln grad"));
     } else {
         for (const char* n : {"text_projection.0.weight", "text_projection.0.bias", "text_projection.2.weight",
@@ -2434,7 +2437,8 @@ int ce_sparc_train_backward(ce_handle* h, void* stream) {
                     sp_grad(h, "visual_projection.2.non_linear_projection.0.weight"), w.gpart));
     CE_TRY(tgemm(h, s, "sparc_bwd_dx", w.dvb, Pd, w.WlT, Pd, N1, Dv, Pd, nullptr, 0, nullptr, w.dh, false, w.gpart));
     CE_TRY(tgemm(h, s, "sparc_bwd_dx", w.da, Pd, w.W1T, Pd, N1, Dv, Pd, nullptr, 0, w.dh, w.dh, false, w.gpart));
-    CE_TRY(check_launch(ce::launch_ln_grad(w.dh, w.xv, w.stv, N1, Dv, p, 2 * seed, sp_grad(h, "visual_projection.0.weight"),
+    CE_TRY(check_launch(ce::launch_ln_grad(w.dh, w.xv, w.stv, N1, Dv, p, 2 * seed, (long)h->sp_sample0 * P,
+                                           sp_grad(h, "visual_projection.0.weight"),
                                            sp_grad(h, "visual_projection.0.bias"), w.lng, s), "sparc ln grad"));
     h->sp_state = 1;    // (a new loss_grad is needed before another backward)
     return CE_OK;

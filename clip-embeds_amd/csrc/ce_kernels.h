@@ -218,13 +218,14 @@ hipError_t launch_f32_to_bf16(bf16_t* out, const float* in, long n, hipStream_t 
 
 // ---- SPARC head training (sparc_train.hip) ----
 // LayerNorm (eps 1e-5) + Dropout(p) per row of D (% 256, <= 1024): out bf16 or f32, stats[r] = (mu, rstd);
-// the keep mask is a counter hash of (seed, r * D + c), recomputed by launch_ln_grad
+// the keep mask is a counter hash of (seed, (roff + r) * D + c) (roff: the global row of local row 0),
+// recomputed by launch_ln_grad
 hipError_t launch_ln_drop(const float* x, const float* w, const float* b, long R, int D, float p, uint64_t seed,
-                          void* out, bool out_bf16, float2* stats, hipStream_t s);
+                          long roff, void* out, bool out_bf16, float2* stats, hipStream_t s);
 // dw, db (overwritten) = the LayerNorm weight / bias gradients through that dropout; scratch >= ln_grad_scratch_floats
 long ln_grad_scratch_floats(long R, int D);
 hipError_t launch_ln_grad(const float* dy, const float* x, const float2* stats, long R, int D, float p, uint64_t seed,
-                          float* dw, float* db, float* scratch, hipStream_t s);
+                          long roff, float* dw, float* db, float* scratch, hipStream_t s);
 // io: d loss / d W in, d loss / d S out, per row of P (sparc weights backward, S = raw similarity)
 hipError_t launch_align_bwd(const float* S, float* io, long rows, int P, float sigma, hipStream_t s);
 // SparcLoss local-term gradient per sample: dR, dR^T [B][T][T] and part[B][3] from R = scale Gn Ln^T (T <= 80)

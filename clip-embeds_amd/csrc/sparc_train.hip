@@ -10,7 +10,9 @@ namespace {
 
 // nn.Dropout(p) keep decision: counter-based, so the backward recomputes the forward's mask.
 // keep(seed, i) = top 24 bits of splitmix64(seed + (i + 1) * gamma) >= p * 2^24 (the generator's
-// n-th output for state seed).  tests/test_gpu_sparc_train.py restates it in NumPy.
+// n-th output for state seed).  i counts elements over the GLOBAL batch (row offset roff = the rank's
+// first sample x rows per sample), so a data-parallel step draws the masks of the single-device step.
+// tests/test_gpu_sparc_train.py restates it in NumPy.
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t i, uint32_t thresh) {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -29,7 +31,7 @@ __host__ __device__ inline uint32_t drop_thresh(float p) {
 template <bool OUT_BF16>
 __global__ __launch_bounds__(256) void ln_drop_k(const float* __restrict__ x, const float* __restrict__ w,
                                                  const float* __restrict__ b, long R, int D, uint32_t thresh,
-                                                 float inv_keep, uint64_t seed, void* __restrict__ out,
+                                                 float inv_keep, uint64_t seed, long roff, void* __restrict__ out,
                                                  float2* __restrict__ stats) {
     const int lane = threadIdx.x & 63;
     const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(256) void ln_drop_k(const float* __restrict__ x, co
                       (v[q].z - mu) * rstd * g.z + bb.z, (v[q].w - mu) * rstd * g.w + bb.w};
         if (thresh) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = drop_keep(seed, (uint64_t)r * D + c0 + e, thresh) ? y[e] * inv_keep : 0.f;
+            for (int e = 0; e < 4; ++e)
+                y[e] = drop_keep(seed, (uint64_t)(roff + r) * D + c0 + e, thresh) ? y[e] * inv_keep : 0.f;
         }
         if constexpr (OUT_BF16) {
             *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + r * D + c0) =
@@ -74,14 +77,14 @@ __global__ __launch_bounds__(256) void ln_drop_k(const float* __restrict__ x, co
 constexpr int LNG_ROWS = 128;
 __global__ __launch_bounds__(256) void ln_grad_part_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                       const float2* __restrict__ stats, long R, int D, uint32_t thresh,
-                                                      float inv_keep, uint64_t seed, float* __restrict__ part) {
+                                                      float inv_keep, uint64_t seed, long roff, float* __restrict__ part) {
     const long r0 = (long)blockIdx.x * LNG_ROWS;
     const long r1 = min(R, r0 + LNG_ROWS);
     for (int c = threadIdx.x; c < D; c += 256) {
         float ag = 0.f, ab = 0.f;
         for (long r = r0; r < r1; ++r) {
             float g = dy[r * D + c];
-            if (thresh) g = drop_keep(seed, (uint64_t)r * D + c, thresh) ? g * inv_keep : 0.f;
+            if (thresh) g = drop_keep(seed, (uint64_t)(roff + r) * D + c, thresh) ? g * inv_keep : 0.f;
             const float2 st = stats[r];
             ag = fmaf(g, (x[r * D + c] - st.x) * st.y, ag);
             ab += g;
@@ -267,25 +270,25 @@ __global__ __launch_bounds__(256) void bcast_add_mid_k(float* __restrict__ x, co
 }  // namespace
 
 hipError_t launch_ln_drop(const float* x, const float* w, const float* b, long R, int D, float p, uint64_t seed,
-                          void* out, bool out_bf16, float2* stats, hipStream_t s) {
+                          long roff, void* out, bool out_bf16, float2* stats, hipStream_t s) {
     if (R <= 0) return hipSuccess;
     if (D % 256 != 0 || D > 1024 || !(p >= 0.f && p < 1.f)) return hipErrorInvalidValue;
     const uint32_t th = drop_thresh(p);
     const float ik = 1.0f / (1.0f - p);
     const dim3 grid((unsigned)((R + 3) / 4));
-    if (out_bf16) hipLaunchKernelGGL(ln_drop_k<true>, grid, dim3(256), 0, s, x, w, b, R, D, th, ik, seed, out, stats);
-    else hipLaunchKernelGGL(ln_drop_k<false>, grid, dim3(256), 0, s, x, w, b, R, D, th, ik, seed, out, stats);
+    if (out_bf16) hipLaunchKernelGGL(ln_drop_k<true>, grid, dim3(256), 0, s, x, w, b, R, D, th, ik, seed, roff, out, stats);
+    else hipLaunchKernelGGL(ln_drop_k<false>, grid, dim3(256), 0, s, x, w, b, R, D, th, ik, seed, roff, out, stats);
     return hipGetLastError();
 }
 
 long ln_grad_scratch_floats(long R, int D) { return ((R + LNG_ROWS - 1) / LNG_ROWS) * 2L * D; }
 
 hipError_t launch_ln_grad(const float* dy, const float* x, const float2* stats, long R, int D, float p, uint64_t seed,
-                          float* dw, float* db, float* scratch, hipStream_t s) {
+                          long roff, float* dw, float* db, float* scratch, hipStream_t s) {
     if (R <= 0) return hipSuccess;
     const int nch = (int)((R + LNG_ROWS - 1) / LNG_ROWS);
     hipLaunchKernelGGL(ln_grad_part_k, dim3((unsigned)nch), dim3(256), 0, s, dy, x, stats, R, D, drop_thresh(p),
-                       1.0f / (1.0f - p), seed, scratch);
+                       1.0f / (1.0f - p), seed, roff, scratch);
     hipLaunchKernelGGL(ln_grad_finish_k, dim3((unsigned)((2 * D + 255) / 256)), dim3(256), 0, s, scratch, nch, D, dw, db);
     return hipGetLastError();
 }

@@ -277,7 +277,9 @@ int ce_loss_combine(ce_handle* h, void* stream, const float* parts, int n_global
  *                                tokens (text_mode 0: through text_projection) or the token embeddings
  *                                themselves (text_mode 1: precomputed / LLM embeddings, no text head);
  *                                Dropout(dropout) after both head LayerNorms with masks from a counter
- *                                hash of seed (dropout 0: eval-mode heads).  Keeps every activation the
+ *                                hash of seed over the element's index in the GLOBAL batch (sample0 =
+ *                                this rank's first sample: the masks do not depend on the sharding;
+ *                                dropout 0: eval-mode heads).  Keeps every activation the
  *                                backward needs; out_v [B,P,Pd], out_l [B,T,Pd] (normalised), out_g
  *                                [B,T,Pd] (normalised grouped patches) as sparc.forward returns them
  *                                (each nullable).  T <= 80.
@@ -294,7 +296,7 @@ int ce_sparc_train_bind(ce_handle* h, const ce_tensor* params, const ce_tensor* 
 int ce_sparc_train_sync_weights(ce_handle* h, void* stream);
 int ce_sparc_train_forward(ce_handle* h, void* stream, const float* patch_tokens, int B, int P, int rope,
                            const float* text, int text_mode, int T, float sigma, float dropout, uint64_t seed,
-                           float* out_v, float* out_l, float* out_g);
+                           int64_t sample0, float* out_v, float* out_l, float* out_g);
 int ce_sparc_train_loss_grad(ce_handle* h, void* stream, const float* img_all, const float* txt_all, int Bg, int row0,
                              const float* mask, float mask_total, float temperature, float global_weight,
                              float local_weight, float* parts);

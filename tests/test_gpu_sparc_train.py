@@ -173,13 +173,13 @@ def _dist_inputs(r):
     return W.synthetic_images(3, seed=1600 + r), l_tok, mask
 
 
-def _dist_trainer(world, rank):
+def _dist_trainer(world, rank, dropout):
     cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
     m = _model(sparc_rope, cfg, W.synthetic_state_dict(cfg))
-    return clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0, rank=rank, world_size=world)
+    return clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=dropout, rank=rank, world_size=world)
 
 
-def _dist_worker(rank, world, port, q):
+def _dist_worker(rank, world, port, q, dropout):
     import os
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -187,7 +187,7 @@ def _dist_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         imgs, l_tok, mask = _dist_inputs(rank)
-        tr = _dist_trainer(world, rank)
+        tr = _dist_trainer(world, rank, dropout)
         before = tr.param.clone()
         loss = tr.compute_grads(torch.from_numpy(imgs).cuda(), l_token_embed=l_tok.cuda(), language_mask=mask.cuda())
         tr.apply_update()
@@ -198,15 +198,17 @@ def _dist_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_ranks_equal_one_rank_on_concatenated_batch():
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_two_ranks_equal_one_rank_on_concatenated_batch(dropout):
     """BASELINE configs[4]'s exchange (train_sparc.py:93: nn.DataParallel, the loss over the gathered
     batch, the replicas' gradients summed): two spawned ranks on cuda:0 over gloo (RCCL on the
     driver's multi-GPU node), 3 samples each, against one rank on the 6 concatenated samples: the same
-    loss, the same summed gradient and the same first Adam step on both ranks."""
+    loss, the same summed gradient and the same first Adam step on both ranks.  With dropout the masks
+    index the global batch, so the two ranks draw the single-device step's masks."""
     import socket
     import torch.multiprocessing as mp
     ins = [_dist_inputs(r) for r in range(2)]
-    tr = _dist_trainer(1, 0)
+    tr = _dist_trainer(1, 0, dropout)
     before = tr.param.clone()
     loss1 = float(tr.compute_grads(torch.from_numpy(np.concatenate([i[0] for i in ins])).cuda(),
                                    l_token_embed=torch.cat([i[1] for i in ins]).cuda(),
@@ -221,7 +223,7 @@ def test_two_ranks_equal_one_rank_on_concatenated_batch():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q, dropout)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -275,7 +277,7 @@ def test_errors(cfg, sd):
         _lib.call("ce_sparc_train_loss_grad", h, s, _ptr(x), _ptr(x), 2, 0, _ptr(x), 1.0, 0.1, 0.5, 1.0, _ptr(x))
     import ctypes
     fwd = lambda P, rope, T, p: _lib.call("ce_sparc_train_forward", h, s, _ptr(x), 2, P, rope, _ptr(t), 0, T, 1 / 576, p,
-                                          ctypes.c_uint64(0), None, None, None)
+                                          ctypes.c_uint64(0), ctypes.c_int64(0), None, None, None)
     with pytest.raises(RuntimeError, match="T <= 80"):
         fwd(576, 1, 81, 0.0)
     with pytest.raises(RuntimeError, match="rope tables"):
