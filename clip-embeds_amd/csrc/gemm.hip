@@ -1075,6 +1075,12 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     };
     set_srd(0);
     auto dma = [&](int buf, int j, bool live) {
+#if defined(CE_ABL_DMA) && CE_ABL_DMA == 2
+        return;                          // timing ablation only (wrong outputs): no operand DMA at all
+#endif
+#if defined(CE_ABL_DMA) && CE_ABL_DMA == 1
+        live = false;                    // timing ablation only: every DMA issued, dropped by the range check
+#endif
         const int kb = live ? dk * BK * 2 : 0x7ffff000;
         char* base = smem + buf * STAGE_BYTES;
         // the row-group offset is made opaque so hipcc forms each DMA's VGPR offset in place
