@@ -104,15 +104,6 @@ struct FoldOps {
 #define CE_STORE_AUX 0
 #endif
 
-// SCHED 11 L2 prefetch (CE_W4_PF, A/B build knob): at the end of each K-tile's B3 every wave issues
-// two dword LDS-DMAs (into a 256-B scratch, data unused) that touch every 128-B row segment of the A
-// and W K-slice two K-tiles past the one the operand DMAs are filling, so the operand DMAs of that
-// K-slice find their lines in the XCD's L2 (~20-25 % of the main loop waits for operand
-// data).  The B2 wait then leaves the two prefetches in flight too: vmcnt(DMA_B2 + 2).
-#ifndef CE_W4_PF
-#define CE_W4_PF 0
-#endif
-
 #ifndef CE_FOLD_PREFETCH
 #define CE_FOLD_PREFETCH 0
 #endif
@@ -1029,9 +1020,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     constexpr int DMA_B2 = 10;
     constexpr int P2 = 64 / DMA_B2;                          // MFMAs per DMA in B2
     constexpr int P3 = 32 / (16 - DMA_B2);                   // and in B3
-    constexpr int NPF = CE_W4_PF ? 2 : 0;                    // L2 prefetch pieces per K-tile per wave
-    constexpr int PF_OFF = 2 * STAGE_BYTES + 4 * W4_SIDE_BYTES;
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES + (CE_W4_PF ? 256 : 0)];
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 4 * W4_SIDE_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1086,12 +1075,6 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
     };
     set_srd(0);
     auto dma = [&](int buf, int j, bool live) {
-#if defined(CE_ABL_DMA) && CE_ABL_DMA == 2
-        return;                          // timing ablation only (wrong outputs): no operand DMA at all
-#endif
-#if defined(CE_ABL_DMA) && CE_ABL_DMA == 1
-        live = false;                    // timing ablation only: every DMA issued, dropped by the range check
-#endif
         const int kb = live ? dk * BK * 2 : 0x7ffff000;
         char* base = smem + buf * STAGE_BYTES;
         // the row-group offset is made opaque so hipcc forms each DMA's VGPR offset in place
@@ -1110,24 +1093,6 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             dk = 0;
             ++dt;
             set_srd(dt);
-        }
-    };
-    // L2 prefetch of K-slice dk + ahead of the DMA stream's tile (dead, dropped by the range check,
-    // past the tile's last K-slice or the workgroup's last step): waves 0-1 the A rows, 2-3 the W rows
-    auto pf = [&](int ahead) __attribute__((always_inline)) {
-        if constexpr (CE_W4_PF) {
-            const bool live = dk + ahead < nk && dt * nk + dk + ahead < nsteps;
-            const int kb = live ? (dk + ahead) * BK * 2 : 0x7ffff000;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = (wave & 1) * 128 + i * 64 + lane;
-                if (wave < 2)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(srdA, (CE_LDS void*)(smem + PF_OFF), 4, row * (int)p.lda * 2,
-                                                             kb, 0, 0);
-                else
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(srdW, (CE_LDS void*)(smem + PF_OFF), 4, row * (int)p.ldw * 2,
-                                                             kb, 0, 0);
-            }
         }
     };
 
@@ -1151,8 +1116,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) dma(1, j, 1 < nsteps);
     advance();
-    pf(1);                                   // (step 3; the K-tiles' B3 prefetch steps 4, 5, ...)
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(16 + NPF) : "memory");
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     barrier();
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1248,12 +1212,11 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_w4pp(GemmParams p) {
             // the epilogue began with vmcnt(0) and B1 ended with a barrier.  Waiting here would also
             // drain every store of that epilogue (vmcnt retires loads, DMAs and stores in issue
             // order), exposing their write latency; skipped, they drain under this tile's MFMAs.
-            if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA_B2 + NPF) : "memory");
+            if (!nowait || kt != 0 || t == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DMA_B2) : "memory");
             barrier();
             // ---- B3: MFMA(set1, rows 4-7); set0 of the next step read under it, and the rest of
             // step g+2's DMAs (buf's last reader was B1, before the first barrier) ----
             B3(so, pre, buf, live);
-            pf(2);
             advance();
             ++g;
         };
