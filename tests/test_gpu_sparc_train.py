@@ -290,3 +290,25 @@ def test_errors(cfg, sd):
     Pn[0] = _tensor_entry(b"visual_projection.0.weight", tr.views["visual_projection.0.weight"])
     with pytest.raises(RuntimeError, match="not bound"):
         _lib.call("ce_sparc_train_bind", h, Pn, Pn, 1)
+
+
+def test_bench_size_step_vs_oracle():
+    """BASELINE configs[4] at the bench's size: full-depth towers, B = 256 images with precomputed
+    text-token embeddings [256, 77, 768] + mask (bench.py --workload sparc), one engine step against
+    the f32 autograd restatement of the heads + SparcLoss on the engine's own tower tokens (dropout
+    off here; the masks are checked at 16 samples above)."""
+    from oracle.sparc_train_torch import TorchSparcTrainStep
+    cfg = get_model_config("ViT-L-14-336")
+    m = _model(sparc, cfg, W.synthetic_state_dict(cfg))
+    tr = clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0)
+    B, T = 256, 77
+    imgs = torch.from_numpy(W.synthetic_images(B, seed=1000)).cuda()
+    gen = torch.Generator(device="cpu").manual_seed(3000)
+    l_tok = (torch.randn(B, T, 768, generator=gen) * 0.5).cuda()
+    eot = torch.randint(6, 42, (B,), generator=gen)
+    mask = (torch.arange(T)[None, :] <= eot[:, None]).float().cuda()
+    loss = float(tr.compute_grads(imgs, l_token_embed=l_tok, language_mask=mask))
+    _, pt = m.clip_model.encode_image(imgs)
+    step = TorchSparcTrainStep({n: v.detach() for n, v in tr.views.items()}, device="cuda")
+    ref_loss, ref_grads, _ = step.loss_and_grads(pt, mask, l_token_embed=l_tok, p=0.0)
+    _vs_oracle(tr, ref_loss, ref_grads, loss, skip=[n for n in HEAD_TENSORS if n.startswith("text_projection")])
