@@ -8,7 +8,7 @@ restructures non-default code leaves the default outputs bit for bit unchanged.
 
 Workloads: the bench batch (B = 256 pooled image + text, pruned and every row, logits), token outputs
 (B = 8), the unfolded f32-stream towers (B = 8), PACL ones / rope-after (B = 64), SPARC forward + loss
-(B = 16), and one NegCLIP training step (64 images + 96 captions: loss, flat gradient, first update).
+(B = 16) and one SPARC head training step (dropout on), and one NegCLIP training step (64 images + 96 captions: loss, flat gradient, first update).
 """
 import argparse
 import hashlib
@@ -82,6 +82,14 @@ def run(out_path):
     v, l, g, mask = sp(imgs[:16], caps[:16])
     loss = SparcLoss(0.1, engine=sp.engine)(v, l, g, mask)
     res.update(sparc_v=digest(v), sparc_l=digest(l), sparc_g=digest(g), sparc_loss=digest(loss.reshape(1)))
+    # one SPARC head training step (round 6; builds without it skip these digests)
+    if hasattr(clipembed, "SparcHeadTrainer"):
+        st = clipembed.SparcHeadTrainer(sp, lr=1e-4, dropout=0.1, seed=5)
+        sloss = st.compute_grads(imgs[:16], caps[:16])
+        res.update(sparc_train_loss=digest(sloss.reshape(1)), sparc_train_grad=digest(st.grad))
+        st.apply_update()
+        res["sparc_train_param_after"] = digest(st.param)
+        del st
     del sp
     torch.cuda.synchronize()
 
