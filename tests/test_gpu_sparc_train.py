@@ -312,3 +312,21 @@ def test_bench_size_step_vs_oracle():
     step = TorchSparcTrainStep({n: v.detach() for n, v in tr.views.items()}, device="cuda")
     ref_loss, ref_grads, _ = step.loss_and_grads(pt, mask, l_token_embed=l_tok, p=0.0)
     _vs_oracle(tr, ref_loss, ref_grads, loss, skip=[n for n in HEAD_TENSORS if n.startswith("text_projection")])
+
+
+def test_trainer_argument_errors(cfg, sd):
+    """SparcHeadTrainer's host checks: exactly one text input; a mask with token embeddings; sparc
+    models only."""
+    m = _model(sparc, cfg, sd)
+    tr = clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0)
+    imgs = torch.from_numpy(W.synthetic_images(2, seed=1)).cuda()
+    caps = torch.from_numpy(W.synthetic_captions(2, seed=2)).cuda()
+    l_tok = torch.zeros(2, 77, 768, device="cuda")
+    with pytest.raises(ValueError, match="one of them"):
+        tr.compute_grads(imgs)
+    with pytest.raises(ValueError, match="one of them"):
+        tr.compute_grads(imgs, caps, l_token_embed=l_tok)
+    with pytest.raises(ValueError, match="language_mask is required"):
+        tr.compute_grads(imgs, l_token_embed=l_tok)
+    with pytest.raises(TypeError, match="sparc"):
+        clipembed.SparcHeadTrainer(m.clip_model)
