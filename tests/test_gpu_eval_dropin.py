@@ -178,3 +178,32 @@ def test_eval_pacl_whatsup(golden):
     s = g["pacl_scores"]
     same, n = _check("pacl", margins, s[:, 0, 0] - s[:, 1, 1], correct, g["pacl_correct"])
     print(f"identical decisions: pacl {same}/{n}")
+
+
+@pytest.mark.parametrize("tag", ["sparc", "sparc_rope"])
+def test_eval_sparc_whatsup(golden, tag):
+    """eval_sparc.py:26-56: prepare_data's PACL transform, model.scoring(1 image, 2 captions, local) for
+    local False and True, correct = s[0][0] > s[1][1]; against the reference's full-depth f32 run
+    (tests/golden/eval_sparc_decisions.npz, make_golden_eval.py sparc).  Margins in 100 x cosine units."""
+    from clipembed.pacl import sparc, sparc_rope
+    g = golden("eval_sparc_decisions")
+    cfg = clipembed.get_model_config("ViT-L-14-336")
+    cls = sparc_rope if tag == "sparc_rope" else sparc
+    model = cls(sigma=1.0 / 576, cfg=cfg, clip_state_dict=W.synthetic_state_dict(cfg))
+    model.load_state_dict(W.synthetic_pacl_heads(cfg.with_pacl(768)))
+    device = torch.device("cuda:0")
+    model.to(device)
+    process = clipembed.prepare_data(base_model="ViT-L-14-336")
+    for local in (False, True):
+        margins, correct = [], []
+        for k in range(len(ITEMS)):
+            input_pixels = process.preprocess_image(pil(k)).unsqueeze(0).to(device)
+            tokenized_text = torch.from_numpy(g["ids"][k]).to(device)
+            with torch.no_grad():
+                s = model.scoring(input_pixels, tokenized_text, local=local)
+            correct.append(1 if s[0][0] > s[1][1] else 0)
+            margins.append(100.0 * float(s[0][0] - s[1][1]))
+        key = f"{tag}_{'local' if local else 'global'}"
+        ref = g[f"{key}_scores"]
+        same, n = _check(key, margins, 100.0 * (ref[:, 0, 0] - ref[:, 1, 1]), correct, g[f"{key}_correct"])
+        print(f"identical decisions: {key} {same}/{n}")
