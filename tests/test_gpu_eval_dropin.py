@@ -207,3 +207,30 @@ def test_eval_sparc_whatsup(golden, tag):
         ref = g[f"{key}_scores"]
         same, n = _check(key, margins, 100.0 * (ref[:, 0, 0] - ref[:, 1, 1]), correct, g[f"{key}_correct"])
         print(f"identical decisions: {key} {same}/{n}")
+
+
+@pytest.mark.parametrize("tag", ["pacl_rope", "pacl_rope_after"])
+def test_eval_pacl_variants_whatsup(golden, tag):
+    """eval_pacl.py:49-57 with the RoPE variants its model path selects (eval_pacl.py:372-377), against
+    the reference's full-depth run (tests/golden/eval_pacl_variants.npz, make_golden_eval.py pacl)."""
+    from clipembed.pacl import open_clip_pacl_rope, open_clip_pacl_rope_after
+    g = golden("eval_pacl_variants")
+    cfg = clipembed.get_model_config("ViT-L-14-336")
+    cls = open_clip_pacl_rope if tag == "pacl_rope" else open_clip_pacl_rope_after
+    model = cls("ViT-L-14-336", clip_state_dict=W.synthetic_state_dict(cfg))
+    model.load_state_dict(W.synthetic_pacl_heads(cfg.with_pacl(768)))
+    device = torch.device("cuda:0")
+    model.to(device)
+    process = clipembed.prepare_data(base_model="ViT-L-14-336")
+    margins, correct = [], []
+    for k in range(len(ITEMS)):
+        input_pixels = process.preprocess_image(pil(k)).unsqueeze(0).to(device)
+        tokenized_text = torch.from_numpy(g["ids"][k]).to(device)
+        with torch.no_grad():
+            image_features, text_features = model(input_pixels, tokenized_text)
+            text_probs = 100.0 * image_features @ text_features.T
+        correct.append(1 if text_probs[0][0] > text_probs[1][1] else 0)
+        margins.append(float(text_probs[0][0] - text_probs[1][1]))
+    s = g[f"{tag}_scores"]
+    same, n = _check(tag, margins, s[:, 0, 0] - s[:, 1, 1], correct, g[f"{tag}_correct"])
+    print(f"identical decisions: {tag} {same}/{n}")
