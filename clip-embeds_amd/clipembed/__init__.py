@@ -8,7 +8,7 @@ from .config import ModelConfig, get_model_config, list_models
 from .model import (CLIP, Engine, create_model, create_model_and_transforms, list_pretrained_tags_by_model,
                     load_checkpoint, load_checkpoint_file, load_state_dict, resize_pos_embed)
 from .train import TextTowerTrainer
-from .sparc_train import SparcHeadTrainer
+from .sparc_train import PaclHeadTrainer, SparcHeadTrainer
 from .tokenizer import SimpleTokenizer, decode, get_tokenizer, tokenize
 from .transforms import image_transform, prepare_data, prepare_data_clip
 from .weights import (synthetic_captions, synthetic_images, synthetic_images_u8, synthetic_pacl_heads,
@@ -21,5 +21,5 @@ __all__ = [
     "create_model_and_transforms", "exported_symbols", "get_model_config", "image_transform", "list_models",
     "list_pretrained_tags_by_model", "load_checkpoint", "load_checkpoint_file", "load_state_dict", "resize_pos_embed", "prepare_data", "prepare_data_clip", "synthetic_captions", "synthetic_images", "synthetic_images_u8",
     "synthetic_pacl_heads", "synthetic_state_dict", "SimpleTokenizer", "tokenize", "decode", "get_tokenizer",
-    "TextTowerTrainer", "SparcHeadTrainer",
+    "TextTowerTrainer", "SparcHeadTrainer", "PaclHeadTrainer",
 ]

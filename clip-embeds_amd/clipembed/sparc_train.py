@@ -33,7 +33,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .model import _ptr, _stream
-from .pacl import _all_gather_rows, sparc
+from .pacl import _all_gather_rows, open_clip_pacl, sparc
 from .train import _tensor_entry
 
 HEAD_TENSORS = ["visual_projection.0.weight", "visual_projection.0.bias",
@@ -50,14 +50,13 @@ class SparcHeadTrainer:
     def __init__(self, model: sparc, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, dropout: float = 0.1, temperature: float = 0.1, seed: int = 0,
                  rank: int = 0, world_size: int = 1):
-        if not isinstance(model, sparc):
-            raise TypeError("SparcHeadTrainer trains the heads of clipembed.pacl.sparc / sparc_rope")
+        self._check_model(model)
         self.model = model
         self.e = model.engine
         self.dev = self.e.device
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.dropout, self.temperature = dropout, temperature
-        self.global_weight, self.local_weight = 0.5, 1.0          # SparcLoss (pacl.py:519-521)
+        self.global_weight, self.local_weight = self._loss_weights()
         self.seed, self.rank, self.world = seed, rank, world_size
         heads = model._heads
         missing = [n for n in HEAD_TENSORS if n not in heads]
@@ -92,6 +91,30 @@ class SparcHeadTrainer:
         self.last_seed = None
         self.parts = torch.zeros(5, device=self.dev, dtype=torch.float32)
 
+    # ------------------------------------------------------------------ model-specific pieces
+    def _check_model(self, model):
+        if not isinstance(model, sparc):
+            raise TypeError("SparcHeadTrainer trains the heads of clipembed.pacl.sparc / sparc_rope")
+
+    def _loss_weights(self):
+        return 0.5, 1.0                                          # SparcLoss (pacl.py:519-521)
+
+    def _text_input(self, caps, l_token_embed):
+        """(text [B, T, E] f32, text_mode): the text tower's tokens through text_projection, or the
+        precomputed token embeddings as they are."""
+        m = self.model
+        if caps is not None:
+            caps = m.clip_model._in(caps, (torch.int64,))
+            _, text = m.clip_model.encode_text(caps)
+            return text, 0, caps
+        return l_token_embed.to(self.dev).float(), 1, None
+
+    def _default_mask(self, B, T):
+        if self._caps is None:
+            raise ValueError("SparcHeadTrainer: language_mask is required with l_token_embed")
+        eots = self._caps.argmax(dim=-1)
+        return (torch.arange(T, device=self.dev).expand(B, -1) <= eots.unsqueeze(1)).float()
+
     # ------------------------------------------------------------------ the step
     def forward(self, images: torch.Tensor, caps: Optional[torch.Tensor] = None,
                 l_token_embed: Optional[torch.Tensor] = None, patch_tokens: Optional[torch.Tensor] = None):
@@ -104,13 +127,7 @@ class SparcHeadTrainer:
         if patch_tokens is None:
             _, patch_tokens = m.clip_model.encode_image(images)
         patch_tokens = patch_tokens.float().contiguous()
-        if caps is not None:
-            caps = m.clip_model._in(caps, (torch.int64,))
-            _, text = m.clip_model.encode_text(caps)
-            mode = 0
-        else:
-            text = l_token_embed.to(self.dev).float()
-            mode = 1
+        text, mode, caps = self._text_input(caps, l_token_embed)
         text = text.contiguous()
         B, P, _ = patch_tokens.shape
         T = text.shape[1]
@@ -126,7 +143,7 @@ class SparcHeadTrainer:
         g = torch.empty(B, T, Pd, device=self.dev, dtype=torch.float32)
         self.last_seed = self.seed + self.step_count
         _lib.call("ce_sparc_train_forward", self.e.h, _stream(self.dev), _ptr(patch_tokens), B, P, m.rope, _ptr(text),
-                  mode, T, float(m.sigma), float(self.dropout), ctypes.c_uint64(self.last_seed), ctypes.c_int64(sample0),
+                  mode, T, float(getattr(m, "sigma", 1.0 / 576)), float(self.dropout), ctypes.c_uint64(self.last_seed), ctypes.c_int64(sample0),
                   _ptr(v), _ptr(l), _ptr(g))
         self._caps = caps
         return v, l, g
@@ -140,10 +157,7 @@ class SparcHeadTrainer:
         B, P, Pd = v.shape
         T = l.shape[1]
         if language_mask is None:
-            if caps is None:
-                raise ValueError("SparcHeadTrainer: language_mask is required with l_token_embed")
-            eots = self._caps.argmax(dim=-1)
-            language_mask = (torch.arange(T, device=self.dev).expand(B, -1) <= eots.unsqueeze(1)).float()
+            language_mask = self._default_mask(B, T)
         mask = language_mask.to(self.dev).float().contiguous()
         gi = torch.empty(B, Pd, device=self.dev, dtype=torch.float32)
         gt = torch.empty_like(gi)
@@ -191,3 +205,43 @@ class SparcHeadTrainer:
         out["visual_projection.2.text_projection.0.weight"] = out["visual_projection.2.linear_projection.0.weight"]
         out["visual_projection.2.text_projection.0.bias"] = out["visual_projection.2.linear_projection.0.bias"]
         return out
+
+
+class PaclHeadTrainer(SparcHeadTrainer):
+    """PACL head training step (train_pacl.py:16-40,106-107: model(images, caps), ClipLoss(temperature=0.1),
+    loss.backward(), torch.optim.Adam(lr=1e-4)) for open_clip_pacl / open_clip_pacl_rope on a frozen CLIP
+    (the reference script's own llm2clip_pacl_rope needs network weights).  The same engine step as
+    SparcHeadTrainer with the PACL forward restated in its terms:
+
+      * image features: visual_projection of the (RoPE'd) patch tokens, summed over the patches with
+        weight 1 (pacl.py:135-145, the ones overwrite) and L2-normalised = normalize(mean over patches),
+        exactly SparcLoss's global image feature;
+      * text features: text_projection of the pooled text embedding (pacl.py:116-118) = SPARC's text
+        head on one token per caption (T = 1, mask 1), normalised;
+      * ClipLoss(temperature) = SparcLoss's global term with global weight 1 and local weight 0
+        (pacl.py:489-514 vs 516-584), so the alignment's gradient is zero and only the global term's
+        gradient reaches the heads.
+
+    open_clip_pacl_rope_after (sigmoid(10 cos) weights of the RoPE'd projections) is not on this path."""
+
+    def _check_model(self, model):
+        from . import _lib as L
+        if isinstance(model, sparc) or not isinstance(model, open_clip_pacl):
+            raise TypeError("PaclHeadTrainer trains the heads of clipembed.pacl.open_clip_pacl / open_clip_pacl_rope")
+        if model.weight_mode != L.CE_PACL_ONES or model.rope == L.CE_ROPE_AFTER:
+            raise NotImplementedError("PaclHeadTrainer: the sigmoid-weighted variants (open_clip_pacl_rope_after) "
+                                      "are not on the training path")
+
+    def _loss_weights(self):
+        return 1.0, 0.0                                          # ClipLoss = the CLIP term alone
+
+    def _text_input(self, caps, l_token_embed):
+        if caps is None or l_token_embed is not None:
+            raise ValueError("PaclHeadTrainer.forward: pass caps (the open_clip_pacl text path)")
+        m = self.model
+        caps = m.clip_model._in(caps, (torch.int64,))
+        pooled = m.clip_model.encode_text(caps)                  # [B, 768] (pacl.py:116-118)
+        return pooled.float().unsqueeze(1), 0, caps
+
+    def _default_mask(self, B, T):
+        return torch.ones(B, T, device=self.dev, dtype=torch.float32)

@@ -2105,7 +2105,7 @@ struct SparcWs {
     int B, P, T, Dv, E, Pd;
     long N1, Nt;
     float *xv, *ylin, *v, *xt, *ht, *l, *Ln, *S, *Wt, *G, *Gn, *mv, *ml, *dgi, *dgt, *R, *dR, *dRT, *part;
-    float *dGn, *dLn, *dG, *dS, *tT, *dv, *dh, *dl, *dlT, *dht, *cs, *lng, *abw, *gpart;
+    float *dGn, *dLn, *dG, *dS, *tT, *dv, *dh, *dl, *dlT, *dht, *cs, *lng, *abw, *gpart, *dmv, *dml;
     float2 *stv, *stt;
     bf16_t *hv, *a, *g, *dvb, *da, *W2T, *WlT, *W1T;
 };
@@ -2132,6 +2132,7 @@ size_t sparc_layout(const ce_handle* h, int B, int P, int T, SparcWs* w, char* b
     t.G = (float*)take(BTD * 4);        t.Gn = (float*)take(BTD * 4);
     t.mv = (float*)take((long)B * Pd * 4); t.ml = (float*)take((long)B * Pd * 4);
     t.dgi = (float*)take((long)B * Pd * 4); t.dgt = (float*)take((long)B * Pd * 4);
+    t.dmv = (float*)take((long)B * Pd * 4); t.dml = (float*)take((long)B * Pd * 4);
     t.R = (float*)take(BTT * 4);        t.dR = (float*)take(BTT * 4);    t.dRT = (float*)take(BTT * 4);
     t.part = (float*)take((long)B * 3 * 4 + 32);
     t.dGn = (float*)take(BTD * 4);      t.dLn = (float*)take(BTD * 4);   t.dG = (float*)take(BTD * 4);
@@ -2359,8 +2360,10 @@ int ce_sparc_train_backward(ce_handle* h, void* stream) {
     // ---- means + normalise (pacl.py:566-567) ----
     CE_TRY(check_launch(ce::launch_mean_mid(w.mv, w.v, B, P, Pd, s), "sparc bwd"));
     CE_TRY(check_launch(ce::launch_mean_mid(w.ml, w.Ln, B, T, Pd, s), "sparc bwd"));
-    float* dmv = w.dR;          // (B x Pd <= B x T x T; dR / dRT are free after ce_sparc_train_loss_grad)
-    float* dml = w.dRT;
+    // (their own buffers: dR / dRT hold B x T x T floats, fewer than B x Pd for T < 28 -- one token per
+    // caption in the PACL step)
+    float* dmv = w.dmv;
+    float* dml = w.dml;
     CE_TRY(check_launch(ce::launch_l2norm_bwd(dmv, w.mv, w.dgi, B, Pd, s), "sparc bwd"));
     CE_TRY(check_launch(ce::launch_l2norm_bwd(dml, w.ml, w.dgt, B, Pd, s), "sparc bwd"));
     CE_TRY(check_launch(ce::launch_bcast_add_mid(w.dLn, dml, B, T, Pd, 1.0f / T, s), "sparc bwd"));

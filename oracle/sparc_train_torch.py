@@ -15,6 +15,7 @@ the reference's own ATen calls and autograd, for the trainable SPARC heads on a 
 Dropout: the reference's model.train() draws torch RNG masks; here the keep-masks are arguments
 (None = dropout off, the module in eval mode), so a test can hand in the engine's own masks.
 The frozen towers' tokens come in as inputs (SparcTokens below restates them from the CLIP forward).
+PACL: pacl_loss_and_grads restates one train_pacl.py step (open_clip_pacl / _rope heads, ClipLoss).
 Imported only by tests/; the product never imports it.
 """
 from __future__ import annotations
@@ -128,6 +129,38 @@ class TorchSparcTrainStep:
         wts = sim / (sim.sum(dim=-1, keepdim=True) + 1e-8)
         g = F.normalize(torch.einsum("btp,bpd->btd", wts, v), p=2, dim=-1)
         return v, F.normalize(l, p=2, dim=-1), g
+
+    def pacl_loss_and_grads(self, patch_tokens, pooled_text, temperature=0.1, p=0.1, keep_v=None, keep_t=None):
+        """One train_pacl.py step's loss and head gradients (train_pacl.py:34-39 on open_clip_pacl /
+        open_clip_pacl_rope, pacl.py:112-145,184-197): the visual head on the (RoPE'd) patch tokens, the
+        ones-weighted patch sum, the text head on the pooled text embedding [B, 768], both
+        L2-normalised, ClipLoss(temperature) (pacl.py:489-514).  keep_t: [B, 768] (or [B, 1, 768])."""
+        for t in self.w.values():
+            t.grad = None
+        w = self.w
+        x = torch.as_tensor(patch_tokens).float().to(self.device).clone()
+        h = self._drop(F.layer_norm(x, (x.shape[-1],), w["visual_projection.0.weight"], w["visual_projection.0.bias"],
+                                    1e-5), keep_v, p)
+        v = F.linear(h, w["visual_projection.2.linear_projection.0.weight"],
+                     w["visual_projection.2.linear_projection.0.bias"])
+        v = v + F.linear(F.gelu(F.linear(h, w["visual_projection.2.non_linear_projection.0.weight"],
+                                         w["visual_projection.2.non_linear_projection.0.bias"])),
+                         w["visual_projection.2.non_linear_projection.2.weight"],
+                         w["visual_projection.2.non_linear_projection.2.bias"])
+        t = torch.as_tensor(pooled_text).float().to(self.device).clone()
+        if keep_t is not None:
+            keep_t = torch.as_tensor(keep_t).reshape(t.shape)
+        ht = self._drop(F.layer_norm(t, (t.shape[-1],), w["text_projection.0.weight"], w["text_projection.0.bias"],
+                                     1e-5), keep_t, p)
+        tp = F.linear(ht, w["text_projection.2.weight"], w["text_projection.2.bias"])
+        img = F.normalize(v.sum(dim=1), dim=-1)
+        txt = F.normalize(tp, dim=-1)
+        li = img @ txt.T / temperature
+        labels = torch.arange(li.shape[0], device=li.device)
+        loss = (F.cross_entropy(li, labels) + F.cross_entropy(li.T, labels)) / 2
+        loss.backward()
+        grads = {n: (t_.grad.detach().clone() if t_.grad is not None else None) for n, t_ in self.w.items()}
+        return float(loss), grads
 
     def loss_and_grads(self, patch_tokens, mask, text_tokens=None, l_token_embed=None, sigma=1.0 / 576,
                        temperature=0.1, p=0.1, keep_v=None, keep_t=None):

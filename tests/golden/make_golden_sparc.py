@@ -11,6 +11,7 @@ outputs only: selected token / patch rows of forward(), both scoring() modes and
     python tests/golden/make_golden_sparc.py fulldepth   ->  tests/golden/sparc_fulldepth.npz (24 + 12 blocks)
     python tests/golden/make_golden_sparc.py dist   ->  tests/golden/sparc_dist.npz
     python tests/golden/make_golden_sparc.py train  ->  tests/golden/sparc_train.npz
+    python tests/golden/make_golden_sparc.py train_pacl  ->  tests/golden/pacl_train.npz
 
 `dist`: the reference SparcLoss(0.1) (train_sparc.py:105) and PACL ClipLoss(0.1) (train_pacl.py:106)
 on the CONCATENATION of two ranks' shards (tests/golden/dist_inputs.py), i.e. the value
@@ -166,10 +167,55 @@ def main_train():
     print("wrote", path, "loss", out["loss"], {k: v.shape for k, v in out.items() if k.startswith("grad/")})
 
 
+def main_train_pacl():
+    """One PACL head training step of train_pacl.py (train_pacl.py:16-40, 106-107: model(images, caps),
+    ClipLoss(temperature=0.1), loss.backward(), torch.optim.Adam(lr = 1e-4).step()) with the
+    open_clip_pacl / open_clip_pacl_rope heads (the ones-weighted patch sum, pacl.py:135-145, 184-197;
+    train_pacl.py's own model, llm2clip_pacl_rope, needs network weights) on 3 images + 3 captions with
+    1-block towers, dropout off as in main_train.  Writes, per variant, the loss, every head gradient
+    (1-d whole, 2-d norms and rows GRAD_ROWS) and the first Adam update of the same entries."""
+    import torch
+    from clipembed import weights as W
+    from clipembed.config import get_model_config
+    torch.set_num_threads(8)
+    torch.use_deterministic_algorithms(True)
+    model_mod, _, pacl_mod = MG.import_reference()
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    clip, _ = MG.build_clip(model_mod, cfg)
+    heads = W.synthetic_pacl_heads(cfg.with_pacl(768))
+    imgs = torch.from_numpy(W.synthetic_images(3, seed=1450))
+    caps = torch.from_numpy(W.synthetic_captions(3, seed=2450))
+    out = {"captions": caps.numpy(), "images_sha": np.array(MG.sha(imgs.numpy()))}
+    for tag, cls in (("pacl", pacl_mod.open_clip_pacl), ("pacl_rope", pacl_mod.open_clip_pacl_rope)):
+        mod = MG.build_pacl(pacl_mod, clip, cls, heads)
+        params = dict(mod.named_parameters())
+        opt = torch.optim.Adam(mod.parameters(), lr=1e-4)
+        opt.zero_grad()
+        a, b = mod(imgs, caps)
+        loss = pacl_mod.ClipLoss(temperature=0.1)(a, b)
+        loss.backward()
+        out[f"{tag}/loss"] = np.float32(loss.item())
+        before = {n: params[n].detach().clone() for n in TRAIN_TENSORS}
+        for n in TRAIN_TENSORS:
+            gr = params[n].grad.numpy()
+            out[f"{tag}/grad_norm/{n}"] = np.float32(np.linalg.norm(gr.astype(np.float64)))
+            out[f"{tag}/grad/{n}"] = gr if gr.ndim == 1 else np.ascontiguousarray(gr[GRAD_ROWS])
+        opt.step()
+        for n in TRAIN_TENSORS:
+            d = (params[n].detach() - before[n]).numpy()
+            out[f"{tag}/update/{n}"] = d if d.ndim == 1 else np.ascontiguousarray(d[GRAD_ROWS])
+        print(tag, "loss", out[f"{tag}/loss"], flush=True)
+    path = os.path.join(HERE, "pacl_train.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["dist"]:
         main_dist()
     elif sys.argv[1:] == ["train"]:
         main_train()
+    elif sys.argv[1:] == ["train_pacl"]:
+        main_train_pacl()
     else:
         main(full_depth=sys.argv[1:] == ["fulldepth"])

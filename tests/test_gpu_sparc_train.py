@@ -330,3 +330,23 @@ def test_trainer_argument_errors(cfg, sd):
         tr.compute_grads(imgs, l_token_embed=l_tok)
     with pytest.raises(TypeError, match="sparc"):
         clipembed.SparcHeadTrainer(m.clip_model)
+
+
+@pytest.mark.parametrize("T", [1, 8])
+def test_few_tokens_vs_oracle(b16, T):
+    """Token counts below 28 (T x T < the head width): the backward's per-sample mean gradients have
+    buffers of their own (they once shared the [B, T, T] local-loss scratch, which overflowed there);
+    precomputed token embeddings with a ragged mask vs the oracle."""
+    from oracle.sparc_train_torch import TorchSparcTrainStep
+    m = b16["m"]
+    tr = clipembed.SparcHeadTrainer(m, lr=1e-4, dropout=0.0)
+    gen = torch.Generator(device="cpu").manual_seed(40 + T)
+    l_tok = (torch.randn(16, T, 768, generator=gen) * 0.5).cuda()
+    mask = torch.ones(16, T, device="cuda")
+    if T > 1:
+        mask[::2, T // 2:] = 0.0
+    loss = float(tr.compute_grads(b16["imgs"], l_token_embed=l_tok, language_mask=mask))
+    step = TorchSparcTrainStep({n: v.detach() for n, v in tr.views.items()}, device="cuda")
+    pv = clipembed.pacl.apply_rope(b16["pt"], engine=m.engine)
+    ref_loss, ref_grads, _ = step.loss_and_grads(pv, mask, l_token_embed=l_tok, p=0.0)
+    _vs_oracle(tr, ref_loss, ref_grads, loss, skip=[n for n in HEAD_TENSORS if n.startswith("text_projection")])

@@ -62,3 +62,33 @@ def test_sparc_train_restatement_matches_reference(golden):
         ours = gv if gv.ndim == 1 else gv[rows]
         assert np.abs(ours - ref).max() <= 1e-4 * (np.abs(ref).max() + 1e-30), n
         np.testing.assert_allclose(np.linalg.norm(gv.astype(np.float64)), g[f"grad_norm/{n}"], rtol=1e-4, err_msg=n)
+
+
+def test_pacl_train_restatement_matches_reference(golden):
+    """Pins the PACL step of oracle/sparc_train_torch.py (pacl_loss_and_grads) to the reference's own
+    train_pacl.py step (tests/golden/pacl_train.npz, make_golden_sparc.py train_pacl: open_clip_pacl and
+    open_clip_pacl_rope on 1-block towers, ClipLoss(0.1), loss.backward(), dropout off)."""
+    import hashlib
+    from oracle.sparc_train_torch import HEAD_TENSORS, SparcTokens, TorchSparcTrainStep, rope_tokens
+    g = golden("pacl_train")
+    cfg = get_model_config("ViT-L-14-336").with_depth(1, 1)
+    imgs = W.synthetic_images(3, seed=1450)
+    assert hashlib.sha256(np.ascontiguousarray(imgs).tobytes()).hexdigest() == str(g["images_sha"])
+    sd = W.synthetic_state_dict(cfg)
+    tok = SparcTokens(sd, cfg)
+    caps = g["captions"]
+    pt = tok.image_tokens(torch.from_numpy(imgs))
+    tt = tok.text_tokens(torch.from_numpy(caps))
+    pooled = tt[torch.arange(3), torch.from_numpy(caps).argmax(-1)] @ torch.as_tensor(sd["text_projection"]).float()
+    rows = [0, 1, 383, 767]
+    for tag, pv in (("pacl", pt), ("pacl_rope", rope_tokens(pt))):
+        step = TorchSparcTrainStep(W.synthetic_pacl_heads(cfg.with_pacl(768)))
+        loss, grads = step.pacl_loss_and_grads(pv, pooled, p=0.0)
+        np.testing.assert_allclose(loss, g[f"{tag}/loss"], rtol=1e-5, err_msg=tag)
+        for n in HEAD_TENSORS:
+            gv = grads[n].numpy()
+            ref = g[f"{tag}/grad/{n}"]
+            ours = gv if gv.ndim == 1 else gv[rows]
+            assert np.abs(ours - ref).max() <= 1e-4 * (np.abs(ref).max() + 1e-30), (tag, n)
+            np.testing.assert_allclose(np.linalg.norm(gv.astype(np.float64)), g[f"{tag}/grad_norm/{n}"], rtol=1e-4,
+                                       err_msg=f"{tag} {n}")
