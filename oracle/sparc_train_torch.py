@@ -160,7 +160,7 @@ class TorchSparcTrainStep:
         loss = (F.cross_entropy(li, labels) + F.cross_entropy(li.T, labels)) / 2
         loss.backward()
         grads = {n: (t_.grad.detach().clone() if t_.grad is not None else None) for n, t_ in self.w.items()}
-        return float(loss), grads
+        return float(loss.detach()), grads
 
     def loss_and_grads(self, patch_tokens, mask, text_tokens=None, l_token_embed=None, sigma=1.0 / 576,
                        temperature=0.1, p=0.1, keep_v=None, keep_t=None):
