@@ -259,12 +259,32 @@ def build_pacl(args, dev, rank, world):
     # train_pacl.py:106: temperature 0.1; N > 1: the global-batch value from sharded rows (all-gather of
     # the features + all-reduce of 5 floats; tests/test_dist_gloo.py, tests/test_gpu_dist_loss.py)
     loss = ClipLoss(0.1, engine=mod.engine, rank=rank, world_size=world)
+    pool_flops = 2.0 * 576 * 768 * (2 if cls.weight_mode else 1)
+
+    if args.pacl_train:
+        # the train_pacl.py:16-40 step with open_clip_pacl's heads: forward (dropout 0.1), ClipLoss, head
+        # backward, Adam(lr 1e-4) (train_pacl.py:106-107)
+        if cls is not open_clip_pacl:
+            raise SystemExit("--pacl-train: the ones-weighted open_clip_pacl heads only")
+        tr = clipembed.PaclHeadTrainer(mod, lr=1e-4, dropout=0.1, temperature=0.1, rank=rank, world_size=world)
+
+        def step():
+            out = tr.compute_grads(imgs, caps)
+            tr.apply_update()
+            return out
+        cfgd = {"workload": "PACL head training step (open_clip_pacl, train_pacl.py): frozen towers, heads in train "
+                            "mode, ClipLoss(0.1), head backward, Adam",
+                "batch_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
+                "exchange": ("RCCL all_gather of the normalised features + all_reduce of the loss sums and the "
+                             "head gradients") if world > 1 else "none"}
+        return dict(engine=mod.engine, step=step, pairs=B, sd=sd, cfg=cfg, prunable=False,
+                    flops_per_pair=FLOPS_PER_PAIR + 2.5 * PACL_HEAD_FLOPS,
+                    metric="PACL image-text pairs/sec ViT-L/14-336 (training)", config=cfgd)
 
     def step():
         oi, ot = mod(imgs, caps)
         return loss(oi, ot)
 
-    pool_flops = 2.0 * 576 * 768 * (2 if cls.weight_mode else 1)
     cfgd = {"workload": f"PACL patch-token forward ({cls.__name__}) + patch alignment/pooling + PACL ClipLoss "
                         "(BASELINE configs[2]: batch 512/GPU bf16)",
             "batch_per_gpu": B, "global_batch": world * B, "image_size": 336, "context_length": 77,
@@ -398,6 +418,8 @@ def main():
     ap.add_argument("--hard", type=int, default=None, help="negclip: hard-negative captions per GPU (default B/2)")
     ap.add_argument("--pacl-mode", choices=["ones", "sigmoid_rope_after"], default="ones")
     ap.add_argument("--sparc-rope", action="store_true")
+    ap.add_argument("--pacl-train", action="store_true",
+                    help="pacl: time the train_pacl.py head training step instead of the forward")
     ap.add_argument("--sparc-forward", action="store_true",
                     help="sparc: time the forward + loss value only (default: the full training step)")
     ap.add_argument("--cpu-batch", type=int, default=8, help="pairs per CPU-baseline run")
